@@ -1,0 +1,314 @@
+"""Generate golden fixtures by running the REFERENCE code in this build container.
+
+Run once here (never on the GPU box — /root/reference does not exist there):
+
+    python tests/golden/make_golden.py
+
+It imports the reference's own `model.py`, `selective_loss.py` and
+`utils/compute_metric.py` from /root/reference (read-only), loads the build's
+seeded weights into `model.UNet_B` via `load_state_dict`, and records inputs and
+outputs of the reference training iteration (`train.py:183-209` composed
+exactly: forward, `BCEWithLogitsLoss` aux loss, `calc_selective_risk_image_b`,
+`Adam.step`). Only data (inputs/expected outputs) is written, as small .npz/.json
+files next to this script. `calc_selective_risk_image_b` calls `.cuda()`
+(`selective_loss.py:73`), so `torch.Tensor.cuda` is patched to identity here.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(REF, "utils"))
+
+torch.Tensor.cuda = lambda self, *a, **k: self  # selective_loss.py:73,77 hard-code .cuda()
+
+import model as ref_model  # noqa: E402  (reference)
+import selective_loss as ref_loss  # noqa: E402  (reference)
+from compute_metric import Evaluator  # noqa: E402  (reference)
+
+import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch  # noqa: E402
+
+torch.set_num_threads(8)
+N_SAMPLES = 64
+
+
+def build_ref(seed, selective, input_type="RGB"):
+    net = ref_model.UNet_B(input_type, selective=selective)
+    sd = net.state_dict()
+    p = L.seeded_params(seed, input_type, selective)
+    assert list(sd.keys()) == L.state_dict_keys(input_type, selective), "state_dict key order drift"
+    new = OrderedDict()
+    for k, v in sd.items():
+        new[k] = torch.tensor(p[k]) if k in p else v
+    net.load_state_dict(new)
+    assert [n for n, _ in net.named_parameters()] == [k for k, *_ in L.param_specs(input_type, selective)]
+    return net
+
+
+def sample_idx(name, numel):
+    h = int(hashlib.sha1(name.encode()).hexdigest()[:8], 16)
+    rng = np.random.Generator(np.random.PCG64(h))
+    return np.sort(rng.choice(numel, size=min(N_SAMPLES, numel), replace=False))
+
+
+def record_tensors(out, prefix, named, full_max=1024):
+    for k, t in named.items():
+        a = t.detach().cpu().numpy().astype(np.float32).ravel()
+        out[f"{prefix}norm/{k}"] = np.float64(np.linalg.norm(a.astype(np.float64)))
+        if a.size <= full_max:
+            out[f"{prefix}full/{k}"] = a
+        else:
+            idx = sample_idx(k, a.size)
+            out[f"{prefix}idx/{k}"] = idx.astype(np.int64)
+            out[f"{prefix}val/{k}"] = a[idx]
+
+
+def ref_step(net, optim, x, lab, selective, lamb, chunks=1):
+    """train.py:194-209 (selective / non-selective), with optional DataParallel emulation."""
+    loss_A = torch.nn.BCEWithLogitsLoss()
+    xs = torch.chunk(x, chunks) if chunks > 1 else [x]
+    outs, saved = [], None
+    for r, xc in enumerate(xs):
+        o = net(xc)
+        outs.append(o if selective else (o,))
+        if chunks > 1 and r == 0:
+            saved = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
+    res = {}
+    output = torch.cat([o[0] for o in outs])
+    if selective:
+        selection = torch.cat([o[1] for o in outs])
+        aux = torch.cat([o[2] for o in outs])
+        aux_loss = loss_A(aux, lab)
+        select_loss, coverage = ref_loss.calc_selective_risk_image_b(output, selection, target=lab, lamb=lamb)
+        loss = aux_loss + select_loss
+        res.update(selection=selection.detach(), aux=aux.detach(), aux_loss=aux_loss.detach(),
+                   select_loss=select_loss.detach(), coverage=coverage.detach())
+    else:
+        loss = loss_A(output, lab)
+    optim.zero_grad()
+    loss.backward()
+    if saved is not None:  # DP keeps only replica 0's BN buffer updates (restored after backward:
+        sd = net.state_dict()  # autograd version-checks the buffers BN read)
+        for k, v in saved.items():
+            sd[k].copy_(v)
+    grads = OrderedDict((n, p.grad.detach().clone()) for n, p in net.named_parameters())
+    optim.step()
+    res.update(output=output.detach(), loss=loss.detach(), grads=grads)
+    return res
+
+
+def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outputs=True, seed=0, data_seed=1):
+    x, lab = make_batch(n, size, seed=data_seed)
+    xt, lt = torch.tensor(x), torch.tensor(lab)
+    torch.manual_seed(0)
+    net = build_ref(seed, selective)
+    net.train()
+    optim = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=0)
+    out = {"meta_n": n, "meta_size": size, "meta_selective": int(selective), "meta_lamb": lamb,
+           "meta_steps": steps, "meta_chunks": chunks, "meta_seed": seed, "meta_data_seed": data_seed}
+    out["x_sha1"] = np.bytes_(hashlib.sha1(x.tobytes()).hexdigest())
+    out["label_sha1"] = np.bytes_(hashlib.sha1(lab.tobytes()).hexdigest())
+    if full_outputs:
+        out["x"] = x
+        out["label"] = lab
+    for s in range(steps):
+        r = ref_step(net, optim, xt, lt, selective, lamb, chunks)
+        pre = f"s{s}/"
+        for k in ("loss", "aux_loss", "select_loss", "coverage"):
+            if k in r:
+                out[pre + k] = np.float64(r[k].item())
+        heads = ["output"] + (["selection", "aux"] if selective else [])
+        for h in heads:
+            a = r[h].numpy().astype(np.float32)
+            if full_outputs:
+                out[pre + h] = a
+            else:
+                flat = a.ravel()
+                idx = sample_idx(h, flat.size)
+                out[pre + h + "_idx"] = idx
+                out[pre + h + "_val"] = flat[idx]
+                out[pre + h + "_sum"] = np.float64(a.astype(np.float64).sum())
+                out[pre + h + "_abssum"] = np.float64(np.abs(a.astype(np.float64)).sum())
+            mask = (1.0 * (1 / (1 + np.exp(-a.astype("float64"))) > 0.5)).astype("uint8")  # train.py:150,153
+            out[pre + h + "_mask_sha1"] = np.bytes_(hashlib.sha1(mask.tobytes()).hexdigest())
+            out[pre + h + "_mask_count"] = np.int64(mask.sum())
+        record_tensors(out, pre + "grad", r["grads"])
+        record_tensors(out, pre + "param", OrderedDict(net.named_parameters()))
+        bufs = OrderedDict((k, v) for k, v in net.state_dict().items() if "running" in k)
+        for k, v in bufs.items():
+            out[pre + "buf/" + k] = v.numpy().astype(np.float32)
+        out[pre + "num_batches_tracked"] = np.int64(net.state_dict()["encoder_layer_1_1.1.num_batches_tracked"].item())
+    path = os.path.join(HERE, fname)
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB)")
+
+
+def eval_fixture(fname, n=4, size=64, seed=0, data_seed=3):
+    """Eval-mode forward (net.eval(), eval.py:156,203-205) with seeded non-trivial BN running
+    statistics: logits + eval masks (fp32 sigmoid, eval.py:175,179) + Evaluator metrics."""
+    x, lab = make_batch(n, size, seed=data_seed)
+    net = build_ref(seed, True)
+    rng = np.random.Generator(np.random.PCG64(1234))
+    sd = net.state_dict()
+    out = {}
+    for k in list(sd.keys()):
+        if k.endswith("running_mean"):
+            sd[k].copy_(torch.tensor(rng.uniform(-0.5, 0.5, sd[k].shape).astype(np.float32)))
+        elif k.endswith("running_var"):
+            sd[k].copy_(torch.tensor(rng.uniform(0.5, 2.0, sd[k].shape).astype(np.float32)))
+        if "running" in k:
+            out["buf/" + k] = sd[k].numpy().copy()
+    # widen the head logits (random init gives std ~0.01) so masks/coverage are non-trivial
+    net.eval()
+    with torch.no_grad():
+        for h in ("conv1x1", "conv_select", "conv_aux"):
+            sd[h + ".weight"].mul_(40.0)
+            sd[h + ".bias"].fill_(0.0)
+        o0, s0, a0 = net(torch.tensor(x))
+        # centre the logits: ~50% positive predictions, ~70% selected pixels
+        for h, t, q in (("conv1x1", o0, 0.5), ("conv_select", s0, 0.3), ("conv_aux", a0, 0.5)):
+            sd[h + ".bias"].fill_(-float(np.quantile(t.numpy(), q)))
+            out["head/" + h + ".weight"] = sd[h + ".weight"].numpy().copy()
+            out["head/" + h + ".bias"] = sd[h + ".bias"].numpy().copy()
+    with torch.no_grad():
+        o, s, a = net(torch.tensor(x))
+    out.update({"x": x, "label": lab, "output": o.numpy(), "selection": s.numpy(), "aux": a.numpy()})
+    o32 = o.numpy()
+    with np.errstate(over="ignore"):
+        p = 1 / (1 + np.exp(-o32))  # eval.py:175 (fp32)
+        sp = 1 / (1 + np.exp(-s.numpy()))
+    pred = (1.0 * (p > 0.5)).astype("uint8")
+    sel = 1.0 * (sp > 0.5)
+    out["pred"] = pred
+    out["select_mask"] = sel.astype("uint8")
+    ev = Evaluator(num_class=2, selective=True)
+    ev.add_batch(lab.astype("uint8"), pred, selection=sel)
+    out["eval_cm_selective"] = ev.confusion_matrix
+    out["eval_miou_selective"] = np.float64(ev.get_mIoU())
+    ev2 = Evaluator(num_class=2, selective=False)
+    ev2.add_batch(lab.astype("uint8"), pred)
+    out["eval_cm"] = ev2.confusion_matrix
+    out["eval_miou"] = np.float64(ev2.get_mIoU())
+    path = os.path.join(HERE, fname)
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB)")
+
+
+def loss_cases():
+    """calc_selective_risk_image_b on bounded and saturated logits."""
+    out = {}
+    rng = np.random.Generator(np.random.PCG64(7))
+    cases = []
+    for i, (scale, shape) in enumerate([(1.0, (2, 8, 8)), (3.0, (2, 16, 16)), (5.0, (2, 16, 16)),
+                                          (0.3, (1, 32, 32)), (20.0, (1, 8, 8))]):
+        o = (rng.normal(0, scale, shape)).astype(np.float32)
+        s = (rng.normal(0.5, scale, shape)).astype(np.float32)
+        t = (rng.random(shape) > 0.5).astype(np.float32)
+        for lamb in (2, 8):
+            ot = torch.tensor(o, requires_grad=True)
+            st = torch.tensor(s, requires_grad=True)
+            loss, cov = ref_loss.calc_selective_risk_image_b(ot, st, torch.tensor(t), lamb=lamb)
+            g = torch.autograd.grad(loss, (ot, st), allow_unused=True)
+            key = f"c{i}_l{lamb}"
+            out[key + "/output"], out[key + "/selection"], out[key + "/target"] = o, s, t
+            out[key + "/loss"] = np.float64(loss.item())
+            out[key + "/coverage"] = np.float64(cov.item())
+            out[key + "/g_output"] = g[0].numpy()
+            out[key + "/g_selection"] = g[1].numpy()
+            cases.append(key)
+            # aux loss reference call (train.py:78,195)
+            bce = torch.nn.BCEWithLogitsLoss()(torch.tensor(o), torch.tensor(t))
+            out[key + "/bce"] = np.float64(bce.item())
+    # low-coverage case: selection logits very negative -> constraint active
+    o = rng.normal(0, 1, (2, 8, 8)).astype(np.float32)
+    s = rng.normal(-3, 1, (2, 8, 8)).astype(np.float32)
+    t = (rng.random((2, 8, 8)) > 0.3).astype(np.float32)
+    ot, st = torch.tensor(o, requires_grad=True), torch.tensor(s, requires_grad=True)
+    loss, cov = ref_loss.calc_selective_risk_image_b(ot, st, torch.tensor(t), lamb=2)
+    g = torch.autograd.grad(loss, (ot, st))
+    out.update({"lowcov/output": o, "lowcov/selection": s, "lowcov/target": t,
+                "lowcov/loss": np.float64(loss.item()), "lowcov/coverage": np.float64(cov.item()),
+                "lowcov/g_output": g[0].numpy(), "lowcov/g_selection": g[1].numpy()})
+    cases.append("lowcov")
+    out["cases"] = np.array(cases)
+    path = os.path.join(HERE, "loss_cases.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}")
+
+
+def bisect_threshold(pred_fn):
+    """Smallest positive fp32 logit x with pred_fn(x) == 1 (bisection over fp32 bit patterns)."""
+    lo, hi = 0, np.float32(1.0).view(np.int32).item()
+    assert pred_fn(np.float32(1.0)) == 1 and pred_fn(np.float32(0.0)) == 0
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if pred_fn(np.int32(mid).view(np.float32)) == 1:
+            hi = mid
+        else:
+            lo = mid
+    return float(np.int32(hi).view(np.float32))
+
+
+def kats():
+    """Notebook known-answer tests re-run through the reference's own calls."""
+    target = torch.tensor([[[1, 0, 1], [1, 1, 1], [0, 0, 1]]], dtype=torch.float32)
+    output = torch.tensor([[[[0, 1, 0], [0, 0, 1], [1, 1, 1]], [[1, 0, 1], [1, 1, 0], [0, 0, 0]]]],
+                          dtype=torch.float32)
+    bce = torch.nn.BCEWithLogitsLoss()(output[:, 1], target).item()
+    ce = torch.nn.CrossEntropyLoss()(output, target.long()).item()
+    m_out = np.array([[[[0, 0, 0], [0, 0, 1], [1, 1, 1]], [[1, 1, 1], [1, 1, 0], [0, 0, 0]]]], np.float32)
+    pred = np.argmax(m_out.transpose(0, 2, 3, 1), axis=-1).astype("uint8")
+    ev = Evaluator(num_class=2, selective=0)
+    ev.add_batch(label=target.numpy().astype("uint8"), pred=pred)
+    prec, rec = ev.get_Precision(), ev.get_Recall()
+    train_thr = bisect_threshold(lambda v: int(1 / (1 + np.exp(-np.array([v]).astype("float64")))[0] > 0.5))
+    with np.errstate(over="ignore"):
+        eval_thr = bisect_threshold(lambda v: int((1 / (1 + np.exp(-np.array([v], np.float32))))[0] > 0.5))
+    data = {
+        "source": "jupyters/chcek_losses.ipynb cells 1,4,9; jupyters/check_metrics.ipynb cells 1-5",
+        "loss_target": target.numpy().tolist(),
+        "loss_output": output.numpy().tolist(),
+        "bce_logits_channel1": bce, "bce_notebook": 0.5243,
+        "ce": ce, "ce_notebook": 0.5355,
+        "metric_output": m_out.tolist(),
+        "cm": ev.confusion_matrix.tolist(), "cm_notebook": [[2, 1], [2, 4]],
+        "acc": ev.get_Pixel_Accuracy(), "acc_class": ev.get_Pixel_Accuracy_Class(),
+        "precision": prec.tolist(), "recall": rec.tolist(),
+        "f1": ev.get_F1_Score(prec, rec).tolist(),
+        "miou": ev.get_mIoU(), "miou_notebook": 0.4857142857142857,
+        "iou_class": ev.get_IoU_Class().tolist(),
+        "param_count_unet_b": sum(p.numel() for p in ref_model.UNet_B("RGB").parameters()),
+        "param_count_unet_b_selective": sum(p.numel() for p in ref_model.UNet_B("RGB", True).parameters()),
+        "param_count_unet_b_gh": sum(p.numel() for p in ref_model.UNet_B("GH").parameters()),
+        "param_count_notebook": 7702977,
+        "state_dict_keys_selective": list(ref_model.UNet_B("RGB", True).state_dict().keys()),
+        "train_threshold_fp32_logit": train_thr,
+        "eval_threshold_fp32_logit": eval_thr,
+    }
+    path = os.path.join(HERE, "kat.json")
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1)
+    print(f"wrote {path}: bce={bce:.4f} ce={ce:.4f} miou={data['miou']:.6f} thr={train_thr!r},{eval_thr!r}")
+
+
+if __name__ == "__main__":
+    kats()
+    loss_cases()
+    step_fixture("step_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
+    step_fixture("step_nosel_n2_64.npz", 2, 64, selective=False, steps=2)
+    step_fixture("step_sel_lamb8_n3_32.npz", 3, 32, selective=True, lamb=8, steps=1)
+    step_fixture("dp_sel_n8_32_c4.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=4)
+    step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=False)
+    eval_fixture("eval_sel_n4_64.npz")
