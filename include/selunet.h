@@ -1,0 +1,211 @@
+/*
+ * selunet.h — C-ABI of the MI355X (gfx950) SelectiveUNet_B training path.
+ *
+ * The reference has no FFI: its boundary is the Python API of `model.UNet_B`
+ * (model.py:18-103), `selective_loss.calc_selective_risk_image_b`
+ * (selective_loss.py:58-85), `torch.nn.BCEWithLogitsLoss` (train.py:78,195) and
+ * `torch.optim.Adam` (train.py:90,209). Every ATen op those dispatch to on the
+ * hot path is replaced by one of the entry points below; the Python host layer
+ * (selectivenet_for_semantic_segmentation_binary_amd/) binds them with ctypes and
+ * keeps the reference's module/function signatures. Each entry point notes the
+ * reference call it replaces.
+ *
+ * Conventions
+ *  - Plain device pointers, sizes and a `hipStream_t` passed as `void*` (the
+ *    caller's current stream). No allocation, no synchronisation, no host copies
+ *    inside any call: all workspaces are caller-owned, so every call is graph-
+ *    capturable.
+ *  - Activations are NHWC (channels contiguous), element type `dtype`
+ *    (SELUNET_F32 or SELUNET_BF16); statistics, losses, weight gradients and
+ *    optimizer state are fp32 (reductions fp64 where noted).
+ *  - Return 0 on success, otherwise a nonzero code; `selunet_last_error()` gives
+ *    the message of the last failing call on this thread.
+ */
+#ifndef SELUNET_H
+#define SELUNET_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SELUNET_F32 = 0, SELUNET_BF16 = 1 };
+
+enum {
+  SELUNET_OK = 0,
+  SELUNET_EINVAL = 1,  /* bad argument (null pointer, size, alignment, unsupported shape) */
+  SELUNET_ELAUNCH = 2, /* HIP launch error */
+};
+
+/* Rows of the GEMM output tile (pixels per workgroup); stats slabs have ceil(M/128) rows. */
+#define SELUNET_GEMM_BM 128
+
+/* One source tensor of an implicit-GEMM operand. The transform
+ * v -> relu?(v*scale[c] + shift[c]) is the folded BatchNorm of the producing
+ * CBR block (model.py:12-13), applied on load; padded positions read 0 after it. */
+typedef struct selunet_source {
+  const void* data;    /* NHWC [n][hs][ws][channels] (layout 0) or NCHW fp32 (layout 1) */
+  const float* scale;  /* per-channel, NULL = identity */
+  const float* shift;
+  int32_t channels;
+  int32_t relu;        /* clamp at 0 after the affine */
+  int32_t layout;      /* 0 NHWC, 1 NCHW (network input only, fp32) */
+  int32_t reserved;
+} selunet_source;
+
+/* A gathered ("im2col without materialisation") matrix G[M][K]:
+ *   row m = (img*h + y)*w + x over an n x h x w pixel grid,
+ *   column k = tap*(C0+C1) + c, c < C0 from src[0] else src[1] (torch.cat((up, skip), 1),
+ *   model.py:83,87,91). taps: 1 = the pixel itself; 9 = 3x3 neighbourhood, zero padded
+ *   (conv 3x3 pad 1, model.py:11); 4 = the 2x2 block (2y+a, 2x+b) of a (2h)x(2w) source grid
+ *   (ConvTranspose2d k2 s2 backward, model.py:44,51,57). */
+typedef struct selunet_gather {
+  int32_t n, h, w;
+  int32_t taps;
+  int32_t nsrc;
+  int32_t reserved;
+  selunet_source src[2];
+} selunet_gather;
+
+enum { SELUNET_EP_PLAIN = 0, SELUNET_EP_SPLIT = 1, SELUNET_EP_SCATTER2X = 2 };
+
+/* Epilogue of selunet_gemm_gather. PLAIN: out0[M][N]; SPLIT: columns < split go to
+ * out0[M][split], the rest to out1[M][N-split] (backward of torch.cat); SCATTER2X:
+ * column (a*2+b)*Cq + c of row (img,y,x) goes to out0[img][2y+a][2x+b][c], Cq = N/4
+ * (ConvTranspose2d k2 s2 forward). bias (fp32, per output channel) is added when
+ * non-NULL. stats (fp32 [ceil(M/128)][2][N]): per-workgroup column sum and sum of
+ * squares of the fp32 accumulators (BatchNorm batch statistics, model.py:12). */
+typedef struct selunet_epilogue {
+  void* out0;
+  void* out1;
+  const float* bias;
+  float* stats;
+  int32_t mode;
+  int32_t split;
+} selunet_epilogue;
+
+const char* selunet_last_error(void);
+int32_t selunet_version(void);
+
+/* ---- weight repacking (fp32 master weights -> GEMM operands, dtype) ---------------- */
+/* conv3x3 weight [co][ci][3][3] -> fwd [co][k_pad] (k = tap*ci + c, zero pad to k_pad) and,
+ * if dgrad != NULL, dgrad [ci][9*co] with the taps flipped (k = tap*co + o). */
+int selunet_pack_conv3x3(const float* w, int32_t co, int32_t ci, int32_t k_pad, void* fwd,
+                         void* dgrad, int32_t dtype, void* stream);
+/* ConvTranspose2d weight [ci][co][2][2] -> fwd [4*co][ci] (row (a*2+b)*co+o) and
+ * dgrad [ci][4*co]. */
+int selunet_pack_convT(const float* w, int32_t ci, int32_t co, void* fwd, void* dgrad,
+                       int32_t dtype, void* stream);
+/* packed fp32 grads -> reference layouts (accumulated into out when accumulate != 0) */
+int selunet_unpack_conv3x3_grad(const float* packed, int32_t co, int32_t ci, int32_t k_pad,
+                                float* out, void* stream);
+int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float* out, void* stream);
+
+/* ---- implicit GEMMs (MFMA) ------------------------------------------------------------ */
+/* out = G_a[M][K] * B^T, B = [n_cols][k_pad] in dtype. Replaces conv2d 3x3 forward and
+ * data-gradient, conv_transpose2d forward and data-gradient (model.py:11,44,51,57). */
+int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
+                        const selunet_epilogue* ep, int32_t dtype, void* stream);
+/* out[ni][nj] += sum_m G_p[m][i] * G_q[m][j] (fp32 atomics; out zeroed by the caller).
+ * Replaces the weight-gradient of conv2d / conv_transpose2d (train.py:208 backward). */
+int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out,
+                       int32_t dtype, void* stream);
+/* Row stride of the packed wgrad output for a Q operand with kq columns (kq rounded up to
+ * the column tile); `out` must be [ni][selunet_wgrad_ld(kq)], the pad columns are garbage-free
+ * zeros when out was zeroed. */
+int32_t selunet_wgrad_ld(int32_t kq);
+
+/* ---- reductions ----------------------------------------------------------------------- */
+/* out[c] = sum_r slab[r][c] in fp64, deterministic order, written as fp64 (out) and/or fp32
+ * (out32), either may be NULL; ws: >= selunet_reduce_ws_bytes(cols). */
+int64_t selunet_reduce_ws_bytes(int32_t cols);
+int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* ws, double* out,
+                        float* out32, void* stream);
+/* per-channel sums of an NHWC tensor: slab [selunet_channel_slab_rows(M)][C] */
+int64_t selunet_channel_slab_rows(int64_t m);
+int selunet_channel_sum(const void* x, int64_t m, int32_t c, float* slab, int32_t dtype, void* stream);
+
+/* ---- BatchNorm2d (model.py:12; eps 1e-5, momentum 0.1) ------------------------------- */
+/* From fp64 sums [2][C] (sum, sumsq of conv output without bias) over `count` pixels:
+ * training: mean/invstd of the batch, running stats updated (unbiased var), *num_batches += 1;
+ * eval (training == 0): running stats. Writes mean (of conv output w/o bias), invstd, and the
+ * folded scale = gamma*invstd, shift = beta - mean*scale used by consumers' loaders. */
+int selunet_bn_finalize(const double* sums, int64_t count, int32_t c, const float* conv_bias,
+                        const float* gamma, const float* beta, float* running_mean,
+                        float* running_var, int64_t* num_batches, float momentum, float eps,
+                        int32_t training, float* mean, float* invstd, float* scale, float* shift,
+                        void* stream);
+/* slab [selunet_channel_slab_rows(M)][3][C]: sum(dA), sum(dA*xhat), sum(xhat), dA = dz*[z>0],
+ * z = relu(y*scale+shift), xhat = (y-mean)*invstd. */
+int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, float* slab,
+                          int32_t dtype, void* stream);
+/* From fp64 sums [3][C]: dgamma, dbeta, dbias (pre-BN conv bias), coef [3][C]. */
+int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const float* gamma,
+                            const float* invstd, float* dgamma, float* dbeta, float* dbias,
+                            float* coef, void* stream);
+/* dy = coef0*dA - coef1 - coef2*xhat (the conv-output gradient). */
+int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
+                         const float* shift, const float* mean, const float* invstd,
+                         const float* coef, void* dy, int32_t dtype, void* stream);
+
+/* ---- MaxPool2d(2) on relu(bn(y)) (model.py:31,35,39) ---------------------------------- */
+int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
+                         const float* scale, const float* shift, void* out, int32_t dtype,
+                         void* stream);
+/* dz = route(dpool to the first max of each window, row-major, strict >) + dskip (nullable). */
+int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
+                         const float* scale, const float* shift, const void* dpool,
+                         const void* dskip, void* dz, int32_t dtype, void* stream);
+
+/* ---- 1x1 heads conv1x1 / conv_select / conv_aux on relu(bn(y)), C = 64 (model.py:62-66) */
+int selunet_heads_fwd(const void* y, int64_t m, const float* scale, const float* shift,
+                      const float* w, const float* b, int32_t nh, float* out0, float* out1,
+                      float* out2, int32_t dtype, void* stream);
+/* dz[m][c] = sum_h g_h[m] w_h[c]; slab [selunet_channel_slab_rows(M)][nh][65]: per head
+ * sum g*z (weight grad, 64) and sum g (bias grad). */
+int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float* shift,
+                      const float* w, int32_t nh, const float* g0, const float* g1,
+                      const float* g2, void* dz, float* slab, int32_t dtype, void* stream);
+
+/* ---- losses ----------------------------------------------------------------------------- */
+/* calc_selective_risk_image_b (selective_loss.py:58-85), numerically stable form.
+ * partials slab [selunet_loss_slab_rows(P)][2]: sum sigmoid(g), sum ell*sigmoid(g). */
+int64_t selunet_loss_slab_rows(int64_t p);
+int selunet_selective_partials(const float* out, const float* sel, const float* target,
+                               int64_t p, float* slab, void* stream);
+/* sums[2] global (after any cross-rank all-reduce), p_global pixels -> loss, coverage,
+ * and state[4] = {S0, R, d, P} for the backward. */
+int selunet_selective_finalize(const double* sums, double p_global, float lamb,
+                               float target_coverage, float* loss, float* coverage,
+                               float* state, void* stream);
+int selunet_selective_bwd(const float* out, const float* sel, const float* target, int64_t p,
+                          const float* state, float lamb, const float* g_loss,
+                          const float* g_coverage, float* d_out, float* d_sel, void* stream);
+/* BCEWithLogitsLoss() mean (train.py:78): slab [selunet_loss_slab_rows(P)][1]. */
+int selunet_bce_partials(const float* logit, const float* target, int64_t p, float* slab,
+                         void* stream);
+int selunet_bce_finalize(const double* sums, double p_global, float* loss, void* stream);
+int selunet_bce_bwd(const float* logit, const float* target, int64_t p, double p_global,
+                    const float* g_loss, float* d_logit, void* stream);
+
+/* ---- torch.optim.Adam (train.py:90,209), multi-tensor ---------------------------------- */
+typedef struct selunet_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  int64_t chunk_begin; /* prefix sum of ceil(numel / SELUNET_ADAM_CHUNK) */
+} selunet_adam_tensor;
+#define SELUNET_ADAM_CHUNK 4096
+/* list: device array of n entries. step: the 1-based step count after increment. */
+int selunet_adam_step(const selunet_adam_tensor* list, int32_t n, int64_t total_chunks, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, int64_t step,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SELUNET_H */

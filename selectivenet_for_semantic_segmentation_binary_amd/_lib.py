@@ -1,0 +1,170 @@
+"""ctypes binding of libselunet.so (the C-ABI declared in include/selunet.h).
+
+The product path has no CPU fallback: if the library is missing or cannot be
+loaded, every entry point raises. Build it with
+``python -m selectivenet_for_semantic_segmentation_binary_amd.build``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from . import build as _build
+
+c_int32, c_int64, c_double, c_float, c_void_p = (ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                                                ctypes.c_float, ctypes.c_void_p)
+
+F32, BF16 = 0, 1
+EP_PLAIN, EP_SPLIT, EP_SCATTER2X = 0, 1, 2
+GEMM_BM = 128
+ADAM_CHUNK = 4096
+
+
+class Source(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("scale", c_void_p), ("shift", c_void_p), ("channels", c_int32),
+                ("relu", c_int32), ("layout", c_int32), ("reserved", c_int32)]
+
+
+class Gather(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("taps", c_int32), ("nsrc", c_int32),
+                ("reserved", c_int32), ("src", Source * 2)]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("out0", c_void_p), ("out1", c_void_p), ("bias", c_void_p), ("stats", c_void_p),
+                ("mode", c_int32), ("split", c_int32)]
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", c_int64), ("chunk_begin", c_int64)]
+
+
+P = c_void_p
+# name -> (restype, argtypes); mirrors include/selunet.h
+SIGNATURES = {
+    "selunet_last_error": (ctypes.c_char_p, []),
+    "selunet_version": (c_int32, []),
+    "selunet_pack_conv3x3": (c_int32, [P, c_int32, c_int32, c_int32, P, P, c_int32, P]),
+    "selunet_pack_convT": (c_int32, [P, c_int32, c_int32, P, P, c_int32, P]),
+    "selunet_unpack_conv3x3_grad": (c_int32, [P, c_int32, c_int32, c_int32, P, P]),
+    "selunet_unpack_convT_grad": (c_int32, [P, c_int32, c_int32, P, P]),
+    "selunet_gemm_gather": (c_int32, [ctypes.POINTER(Gather), P, c_int32, c_int32, ctypes.POINTER(Epilogue),
+                                      c_int32, P]),
+    "selunet_gemm_wgrad": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int32, P]),
+    "selunet_wgrad_ld": (c_int32, [c_int32]),
+    "selunet_reduce_ws_bytes": (c_int64, [c_int32]),
+    "selunet_reduce_rows": (c_int32, [P, c_int64, c_int32, P, P, P, P]),
+    "selunet_channel_slab_rows": (c_int64, [c_int64]),
+    "selunet_channel_sum": (c_int32, [P, c_int64, c_int32, P, c_int32, P]),
+    "selunet_bn_finalize": (c_int32, [P, c_int64, c_int32, P, P, P, P, P, P, c_float, c_float, c_int32, P, P, P, P,
+                                      P]),
+    "selunet_bn_bwd_reduce": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_bn_bwd_finalize": (c_int32, [P, c_int64, c_int32, P, P, P, P, P, P, P]),
+    "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
+    "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
+    "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),
+    "selunet_heads_bwd": (c_int32, [P, c_int64, P, P, P, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_loss_slab_rows": (c_int64, [c_int64]),
+    "selunet_selective_partials": (c_int32, [P, P, P, c_int64, P, P]),
+    "selunet_selective_finalize": (c_int32, [P, c_double, c_float, c_float, P, P, P, P]),
+    "selunet_selective_bwd": (c_int32, [P, P, P, c_int64, P, c_float, P, P, P, P, P]),
+    "selunet_bce_partials": (c_int32, [P, P, c_int64, P, P]),
+    "selunet_bce_finalize": (c_int32, [P, c_double, P, P]),
+    "selunet_bce_bwd": (c_int32, [P, P, c_int64, c_double, P, P, P]),
+    "selunet_adam_step": (c_int32, [P, c_int32, c_int64, c_float, c_float, c_float, c_float, c_float, c_int64, P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(auto_build: bool = False):
+    """Load (optionally build) libselunet.so; raise RuntimeError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not os.path.exists(path):
+            if auto_build:
+                _build.build(verbose=False)
+            else:
+                raise RuntimeError(
+                    f"{path} not found: the MI355X kernels are not built (run "
+                    "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`). "
+                    "There is no CPU fallback.")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class SelunetError(RuntimeError):
+    pass
+
+
+_HOOK = None
+
+
+def set_call_hook(hook):
+    """Install hook(name, args, fn) -> rc around every entry-point call (profiling), None to clear."""
+    global _HOOK
+    _HOOK = hook
+
+
+def call(name, *args):
+    L = load()
+    fn = getattr(L, name)
+    rc = fn(*args) if _HOOK is None else _HOOK(name, args, lambda: fn(*args))
+    if rc != 0:
+        raise SelunetError(f"{name}: {L.selunet_last_error().decode()}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+# ----------------------------------------------------------------------------- tensor helpers
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise ValueError(f"unsupported activation dtype {dt}")
+
+
+def source(data, channels, scale=None, shift=None, relu=True, layout=0) -> Source:
+    return Source(ptr(data), ptr(scale), ptr(shift), channels, int(bool(relu) and scale is not None), layout, 0)
+
+
+def gather(n, h, w, taps, *srcs: Source) -> Gather:
+    g = Gather(n, h, w, taps, len(srcs), 0)
+    for i, s in enumerate(srcs):
+        g.src[i] = s
+    return g

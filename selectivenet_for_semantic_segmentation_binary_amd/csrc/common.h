@@ -1,0 +1,71 @@
+// Shared device/host helpers for the gfx950 SelectiveUNet_B kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/selunet.h"
+
+namespace selunet {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ error state (host)
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+#define SELUNET_REQUIRE(cond, ...)                         \
+  do {                                                     \
+    if (!(cond)) return ::selunet::fail(SELUNET_EINVAL, __VA_ARGS__); \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------------------ element access
+// 4 consecutive elements <-> float4 in registers.
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  __device__ static inline f32x4 load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  __device__ static inline void store(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+};
+template <> struct Vec4<__bf16> {
+  __device__ static inline f32x4 load(const __bf16* p) {
+    bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+  __device__ static inline void store(__bf16* p, f32x4 v) {
+    bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = o;
+  }
+};
+
+template <typename T> __device__ inline float to_f(T v) { return (float)v; }
+template <typename T> __device__ inline T from_f(float v) { return (T)v; }
+
+__device__ inline float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// numerically stable softplus(x) = log(1 + exp(x))
+__device__ inline float softplusf_(float x) { return fmaxf(x, 0.0f) + log1pf(__expf(-fabsf(x))); }
+
+// wave64 sum
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace selunet

@@ -1,0 +1,805 @@
+// Implicit-GEMM MFMA kernels for the UNet_B convolutions on gfx950.
+//
+//  * gemm_gather: out[M][N] = G[M][K] * B[N][K]^T, where G is a gathered view of one or two
+//    NHWC activations (3x3 / 1x1 / 2x2-stride-2 taps, channel concat) with the producing
+//    block's BatchNorm+ReLU folded into the load. Used for conv3x3 forward (model.py:11),
+//    conv3x3 data-gradient, ConvTranspose2d forward (model.py:44,51,57) and its
+//    data-gradient. Epilogue: NHWC store (plain / cat-split / 2x scatter + bias) and the
+//    per-workgroup BatchNorm column statistics of the fp32 accumulators.
+//  * gemm_wgrad: out[I][J] += sum_m Gp[m][I] * Gq[m][J] — weight gradients, the reduction
+//    over pixels split across workgroups, fp32 atomics into a packed buffer.
+//
+// Tiling (256 threads = 4 waves as 2x2, 64-wide wavefronts): 128 x BN output tile, one
+// 128-byte K slice per stage (32 fp32 / 64 bf16), register-staged double-buffered LDS with
+// the next slice's global loads in flight during the current slice's MFMAs (load early,
+// write late). Rows of the LDS tiles are padded to 144 B so that the 16-B fragment reads
+// (ds_read_b128) of 16 consecutive rows fall on 16 distinct bank slots.
+//  fp32: v_mfma_f32_32x32x2_f32 (exact fp32); each 16-B fragment holds 4 k's of one half-wave,
+//        consumed by 4 MFMAs (k = 4*half + j), B uses the same k assignment.
+//  bf16: v_mfma_f32_32x32x16_bf16; a 16-B fragment is the 8 k's of one half-wave.
+#include <type_traits>
+
+#include "common.h"
+
+namespace selunet {
+
+struct SrcArg {
+  const void* data;
+  const float* scale;
+  const float* shift;
+  int C;
+  int relu;
+  int layout;
+  int pad;
+};
+
+struct GatherArg {
+  int n, h, w;       // row grid
+  int taps;          // 1, 4, 9
+  int nsrc;
+  int Ctot;          // C0 + C1
+  int hs, ws;        // source grid
+  int K;             // taps * Ctot (true K)
+  int small;         // element-wise gather (channels not a multiple of the staging vector)
+  int64_t M;
+  SrcArg src[2];
+};
+
+constexpr int BM = SELUNET_GEMM_BM;
+constexpr int ROWB = 144;  // padded LDS row bytes for a 128-B K slice
+
+// --------------------------------------------------------------------------- gather helpers
+__device__ inline void tap_offset(int taps, int tap, int& dy, int& dx) {
+  if (taps == 9) {
+    dy = tap / 3 - 1;
+    dx = tap - (tap / 3) * 3 - 1;
+  } else if (taps == 4) {
+    dy = tap >> 1;
+    dx = tap & 1;
+  } else {
+    dy = 0;
+    dx = 0;
+  }
+}
+
+// source pixel of row pixel (y, x) for `tap`; returns false when it falls into the zero pad.
+__device__ inline bool src_pixel(const GatherArg& g, int tap, int y, int x, int& ys, int& xs) {
+  int dy, dx;
+  tap_offset(g.taps, tap, dy, dx);
+  if (g.taps == 4) {
+    ys = 2 * y + dy;
+    xs = 2 * x + dx;
+    return true;
+  }
+  ys = y + dy;
+  xs = x + dx;
+  return (unsigned)ys < (unsigned)g.hs && (unsigned)xs < (unsigned)g.ws;
+}
+
+// One gathered element (slow path, small C / non-vector channel counts). Applies the transform.
+template <typename T>
+__device__ inline float gather_scalar(const GatherArg& g, int64_t m, int k) {
+  if (m >= g.M || k >= g.K) return 0.0f;
+  const int tap = k / g.Ctot;
+  int c = k - tap * g.Ctot;
+  int s = 0;
+  if (g.nsrc > 1 && c >= g.src[0].C) {
+    c -= g.src[0].C;
+    s = 1;
+  }
+  const int x = (int)(m % g.w);
+  const int64_t t = m / g.w;
+  const int y = (int)(t % g.h);
+  const int img = (int)(t / g.h);
+  int ys, xs;
+  if (!src_pixel(g, tap, y, x, ys, xs)) return 0.0f;
+  const SrcArg& sa = g.src[s];
+  float v;
+  if (sa.layout == 1) {
+    v = reinterpret_cast<const float*>(sa.data)[(((int64_t)img * sa.C + c) * g.hs + ys) * g.ws + xs];
+  } else {
+    v = to_f(reinterpret_cast<const T*>(sa.data)[(((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c]);
+  }
+  if (sa.scale) {
+    v = v * sa.scale[c] + sa.shift[c];
+    if (sa.relu) v = fmaxf(v, 0.0f);
+  }
+  return v;
+}
+
+// --------------------------------------------------------------------------- MFMA wrappers
+template <typename T> struct Mma;
+template <> struct Mma<float> {
+  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<__bf16> {
+  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
+    bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    bf16x8 bv = __builtin_bit_cast(bf16x8, b);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+  }
+};
+
+// apply folded BN + ReLU to a 16-B vector of T (E elements), channel base c
+template <typename T>
+__device__ inline uint4 transform16(uint4 raw, const float* scale, const float* shift, int c, int relu) {
+  constexpr int E = 16 / sizeof(T);
+  T v[E];
+  __builtin_memcpy(v, &raw, 16);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float f = to_f(v[e]) * scale[c + e] + shift[c + e];
+    if (relu) f = fmaxf(f, 0.0f);
+    v[e] = from_f<T>(f);
+  }
+  uint4 out;
+  __builtin_memcpy(&out, v, 16);
+  return out;
+}
+
+// =========================================================================== gemm_gather
+struct EpiArg {
+  void* out0;
+  void* out1;
+  const float* bias;
+  float* stats;
+  int mode;
+  int split;
+};
+
+template <typename T, int BN>
+__global__ void __launch_bounds__(256, 2)
+gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles) {
+  constexpr int E = 16 / sizeof(T);          // elements per 16-B vector
+  constexpr int BKE = 128 / sizeof(T);       // K elements per stage
+  constexpr int WN = BN / 2;                 // wave tile columns
+  constexpr int NT = WN / 32;                // 32x32 subtiles per wave (columns)
+  constexpr int MT = 2;                      // 64 rows per wave
+  constexpr int AR = BM / 32;                // A rows staged per thread
+  constexpr int BR = BN / 32;                // B rows staged per thread
+
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * ROWB];
+  unsigned char* As = smem;                          // [2][BM][ROWB]
+  unsigned char* Bs = smem + 2 * BM * ROWB;          // [2][BN][ROWB]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const int n_tile = blockIdx.x % n_tiles;
+  const int64_t m_tile = blockIdx.x / n_tiles;
+  const int64_t m0 = m_tile * BM;
+  const int n0 = n_tile * BN;
+
+  const int cc = tid & 7;       // 16-B chunk within the 128-B K slice
+  const int rr = tid >> 3;      // base row (0..31)
+
+  // per-thread row coordinates of the A rows it stages
+  int ry[AR], rx[AR], rimg[AR];
+  bool rv[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int64_t m = m0 + rr + 32 * i;
+    rv[i] = m < g.M;
+    const int64_t mm = rv[i] ? m : 0;
+    rx[i] = (int)(mm % g.w);
+    const int64_t t = mm / g.w;
+    ry[i] = (int)(t % g.h);
+    rimg[i] = (int)(t / g.h);
+  }
+
+  uint4 ra[AR];
+  bool rok[AR];
+  uint4 rb[BR];
+  int st_src = 0, st_c = 0;  // transform selector of the staged slice
+
+  auto load_stage = [&](int kc) {
+    const int k0 = kc * BKE;
+    if (!g.small) {
+      const int tap = k0 / g.Ctot;
+      int c0 = k0 - tap * g.Ctot;
+      int s = 0;
+      if (g.nsrc > 1 && c0 >= g.src[0].C) {
+        c0 -= g.src[0].C;
+        s = 1;
+      }
+      st_src = s;
+      st_c = c0 + cc * E;
+      const SrcArg& sa = g.src[s];
+      const T* base = reinterpret_cast<const T*>(sa.data);
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        int ys, xs;
+        const bool ok = rv[i] && src_pixel(g, tap, ry[i], rx[i], ys, xs);
+        rok[i] = ok;
+        if (ok) {
+          const int64_t off = (((int64_t)rimg[i] * g.hs + ys) * g.ws + xs) * sa.C + st_c;
+          ra[i] = *reinterpret_cast<const uint4*>(base + off);
+        } else {
+          ra[i] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        T v[E];
+        const int64_t m = m0 + rr + 32 * i;
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = from_f<T>(gather_scalar<T>(g, m, k0 + cc * E + e));
+        __builtin_memcpy(&ra[i], v, 16);
+        rok[i] = true;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + rr + 32 * i;
+      rb[i] = *reinterpret_cast<const uint4*>(B + (int64_t)n * k_pad + k0 + cc * E);
+    }
+  };
+
+  auto store_stage = [&](int buf) {
+    unsigned char* a_dst = As + buf * BM * ROWB;
+    unsigned char* b_dst = Bs + buf * BN * ROWB;
+    const SrcArg& sa = g.src[st_src];
+    const bool xf = !g.small && sa.scale != nullptr;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = ra[i];
+      if (xf) v = rok[i] ? transform16<T>(v, sa.scale, sa.shift, st_c, sa.relu) : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(b_dst + (rr + 32 * i) * ROWB + cc * 16) = rb[i];
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  const int nk = k_pad / BKE;
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) load_stage(kc + 1);
+    const unsigned char* a_src = As + buf * BM * ROWB;
+    const unsigned char* b_src = Bs + buf * BN * ROWB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int boff = q * 32 + half * 16;
+      uint4 af[MT], bfr[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+        af[a] = *reinterpret_cast<const uint4*>(a_src + (wm * 64 + a * 32 + l32) * ROWB + boff);
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * WN + b * 32 + l32) * ROWB + boff);
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+    }
+    if (kc + 1 < nk) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  const int Cq = N >> 2;
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int col = n0 + wn * WN + b * 32 + l32;
+      float bias = 0.0f;
+      if (ep.bias) bias = ep.bias[ep.mode == SELUNET_EP_SCATTER2X ? (col % Cq) : col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const int64_t m = m0 + row;
+        if (m >= g.M) continue;
+        const float v = acc[a][b][r] + bias;
+        if (ep.mode == SELUNET_EP_PLAIN) {
+          reinterpret_cast<T*>(ep.out0)[m * N + col] = from_f<T>(v);
+        } else if (ep.mode == SELUNET_EP_SPLIT) {
+          if (col < ep.split)
+            reinterpret_cast<T*>(ep.out0)[m * ep.split + col] = from_f<T>(v);
+          else
+            reinterpret_cast<T*>(ep.out1)[m * (N - ep.split) + (col - ep.split)] = from_f<T>(v);
+        } else {
+          const int ab = col / Cq, c = col - ab * Cq;
+          const int x = (int)(m % g.w);
+          const int64_t t = m / g.w;
+          const int y = (int)(t % g.h);
+          const int64_t img = t / g.h;
+          const int64_t o = ((img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + c;
+          reinterpret_cast<T*>(ep.out0)[o] = from_f<T>(v);
+        }
+      }
+    }
+  }
+
+  if (ep.stats) {
+    // column sum / sum of squares over this workgroup's valid rows (fp32 accumulators)
+    float* red = reinterpret_cast<float*>(smem);  // [2][BN][2], LDS free after the final barrier
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (m0 + row < g.M) {
+            const float v = acc[a][b][r];
+            s1 += v;
+            s2 += v * v;
+          }
+        }
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (half == 0) {
+        const int col = wn * WN + b * 32 + l32;
+        red[(wm * BN + col) * 2 + 0] = s1;
+        red[(wm * BN + col) * 2 + 1] = s2;
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float s1 = red[(0 * BN + tid) * 2 + 0] + red[(1 * BN + tid) * 2 + 0];
+      const float s2 = red[(0 * BN + tid) * 2 + 1] + red[(1 * BN + tid) * 2 + 1];
+      ep.stats[(m_tile * 2 + 0) * N + n0 + tid] = s1;
+      ep.stats[(m_tile * 2 + 1) * N + n0 + tid] = s2;
+    }
+  }
+}
+
+// =========================================================================== gemm_wgrad
+// out[I][J] += sum_m P[m][i] Q[m][j]; fp32 operands via v_mfma_f32_32x32x2_f32. LDS tiles are
+// [32 rows (m)][BI or BJ] fp32 so the MFMA operands (one element per lane: A[i][k], B[k][j])
+// are single conflict-free ds_read_b32 along a row.
+template <typename T>
+__device__ inline f32x4 gather_vec4(const GatherArg& g, int64_t m, int k, int tap, int s, int c,
+                                    bool vec) {
+  if (!vec) {
+    return f32x4{gather_scalar<T>(g, m, k), gather_scalar<T>(g, m, k + 1), gather_scalar<T>(g, m, k + 2),
+                 gather_scalar<T>(g, m, k + 3)};
+  }
+  if (m >= g.M) return f32x4{0, 0, 0, 0};
+  const int x = (int)(m % g.w);
+  const int64_t t = m / g.w;
+  const int y = (int)(t % g.h);
+  const int img = (int)(t / g.h);
+  int ys, xs;
+  if (!src_pixel(g, tap, y, x, ys, xs)) return f32x4{0, 0, 0, 0};
+  const SrcArg& sa = g.src[s];
+  f32x4 v = Vec4<T>::load(reinterpret_cast<const T*>(sa.data) + (((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c);
+  if (sa.scale) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float f = v[e] * sa.scale[c + e] + sa.shift[c + e];
+      v[e] = sa.relu ? fmaxf(f, 0.0f) : f;
+    }
+  }
+  return v;
+}
+
+template <typename T, int BI, int BJ>
+__global__ void __launch_bounds__(256, 2)
+gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk,
+                  int tiles_j, int tiles) {
+  constexpr int KM = 32;              // pixels per stage
+  constexpr int WI = BI / 2, WJ = BJ / 2;
+  constexpr int MT = WI / 32, NT = WJ / 32;
+  constexpr int CPI = BI / 4, CPJ = BJ / 4;       // float4 chunks per row
+  constexpr int RPI = 256 / CPI, RPJ = 256 / CPJ; // rows per pass
+  constexpr int PI = KM / RPI, PJ = KM / RPJ;     // passes
+
+  __shared__ __attribute__((aligned(16))) float Ps[2][KM][BI];
+  __shared__ __attribute__((aligned(16))) float Qs[2][KM][BJ];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const int tile = blockIdx.x % tiles;
+  const int64_t split = blockIdx.x / tiles;
+  const int i0 = (tile / tiles_j) * BI;
+  const int j0 = (tile % tiles_j) * BJ;
+  const int64_t mb = split * mchunk;
+  const int64_t me = min(P.M, mb + mchunk);
+  if (mb >= me) return;
+
+  // fixed column chunk of this thread -> (tap, source, channel) for P and Q
+  const int pc = tid % CPI, pr = tid / CPI;
+  const int qc = tid % CPJ, qr = tid / CPJ;
+  const int pk = i0 + pc * 4, qk = j0 + qc * 4;
+  int ptap = 0, ps = 0, pch = 0, qtap = 0, qs = 0, qch = 0;
+  const bool pvec = !P.small, qvec = !Q.small;
+  if (pvec) {
+    ptap = pk / P.Ctot;
+    pch = pk - ptap * P.Ctot;
+    if (P.nsrc > 1 && pch >= P.src[0].C) { pch -= P.src[0].C; ps = 1; }
+  }
+  if (qvec) {
+    qtap = qk / Q.Ctot;
+    qch = qk - qtap * Q.Ctot;
+    if (Q.nsrc > 1 && qch >= Q.src[0].C) { qch -= Q.src[0].C; qs = 1; }
+  }
+  const bool pin = pk < P.K, qin = qk < Q.K;
+
+  f32x4 rp[PI], rq[PJ];
+  auto load_stage = [&](int64_t m_base) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int64_t m = m_base + pr + RPI * i;
+      rp[i] = (pin && m < me) ? gather_vec4<T>(P, m, pk, ptap, ps, pch, pvec) : f32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < PJ; ++i) {
+      const int64_t m = m_base + qr + RPJ * i;
+      rq[i] = (qin && m < me) ? gather_vec4<T>(Q, m, qk, qtap, qs, qch, qvec) : f32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) *reinterpret_cast<f32x4*>(&Ps[buf][pr + RPI * i][pc * 4]) = rp[i];
+#pragma unroll
+    for (int i = 0; i < PJ; ++i) *reinterpret_cast<f32x4*>(&Qs[buf][qr + RPJ * i][qc * 4]) = rq[i];
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  const int64_t nst = (me - mb + KM - 1) / KM;
+  load_stage(mb);
+  store_stage(0);
+  __syncthreads();
+  for (int64_t st = 0; st < nst; ++st) {
+    const int buf = (int)(st & 1);
+    if (st + 1 < nst) load_stage(mb + (st + 1) * KM);
+#pragma unroll
+    for (int kk = 0; kk < KM / 2; ++kk) {
+      const int row = 2 * kk + half;
+      float av[MT], bv[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) av[a] = Ps[buf][row][wi * WI + a * 32 + l32];
+#pragma unroll
+      for (int b = 0; b < NT; ++b) bv[b] = Qs[buf][row][wj * WJ + b * 32 + l32];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    if (st + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int j = j0 + wj * WJ + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * WI + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
+      }
+    }
+}
+
+// =========================================================================== gemm_wgrad (bf16)
+// Same contraction with v_mfma_f32_32x32x16_bf16. The LDS tiles stay in their natural gathered
+// layout [pixel m][column] (coalesced staging); the MFMA operands need 8 consecutive m per
+// column, which ds_read_b64_tr_b16 delivers: per 16-lane group it reads a 4(m) x 16(col) block
+// and hands lane j column j's 4 values, so two reads give lane (col = l & 31, half = l >> 5)
+// the k-run m = 8*half .. 8*half+7 of its column. Rows are padded by 64 B so the 32 lanes of a
+// read touch 64 distinct banks (row stride = 16 dwords mod 64).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline uint4 gather_vec8_bf16(const GatherArg& g, int64_t m, int k, int tap, int s, int c, bool vec,
+                                         bool in) {
+  if (!in || m >= g.M) return make_uint4(0, 0, 0, 0);
+  if (!vec) {
+    __bf16 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)gather_scalar<__bf16>(g, m, k + e);
+    uint4 o;
+    __builtin_memcpy(&o, v, 16);
+    return o;
+  }
+  const int x = (int)(m % g.w);
+  const int64_t t = m / g.w;
+  const int y = (int)(t % g.h);
+  const int img = (int)(t / g.h);
+  int ys, xs;
+  if (!src_pixel(g, tap, y, x, ys, xs)) return make_uint4(0, 0, 0, 0);
+  const SrcArg& sa = g.src[s];
+  uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(sa.data) +
+                                              (((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c);
+  if (sa.scale) raw = transform16<__bf16>(raw, sa.scale, sa.shift, c, sa.relu);
+  return raw;
+}
+
+template <int BI, int BJ>
+__global__ void __launch_bounds__(256, 2)
+gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk, int tiles_j,
+                       int tiles) {
+  constexpr int KM = 64;                           // pixels per stage
+  constexpr int PADE = 32;                         // 64 B row pad (bank spread for tr reads)
+  constexpr int LDI = BI + PADE, LDJ = BJ + PADE;  // row strides in elements
+  constexpr int WI = BI / 2, WJ = BJ / 2;
+  constexpr int MT = WI / 32, NT = WJ / 32;
+  constexpr int CPI = BI / 8, CPJ = BJ / 8;        // 16-B chunks per row
+  constexpr int RPI = 256 / CPI, RPJ = 256 / CPJ;
+  constexpr int PI = KM / RPI, PJ = KM / RPJ;
+
+  __shared__ __attribute__((aligned(16))) unsigned short Ps[2][KM][LDI];
+  __shared__ __attribute__((aligned(16))) unsigned short Qs[2][KM][LDJ];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  const int tile = blockIdx.x % tiles;
+  const int64_t split = blockIdx.x / tiles;
+  const int i0 = (tile / tiles_j) * BI;
+  const int j0 = (tile % tiles_j) * BJ;
+  const int64_t mb = split * mchunk;
+  const int64_t me = min(P.M, mb + mchunk);
+  if (mb >= me) return;
+
+  const int pc = tid % CPI, pr = tid / CPI;
+  const int qc = tid % CPJ, qr = tid / CPJ;
+  const int pk = i0 + pc * 8, qk = j0 + qc * 8;
+  int ptap = 0, ps = 0, pch = 0, qtap = 0, qs = 0, qch = 0;
+  const bool pvec = !P.small, qvec = !Q.small;
+  if (pvec) {
+    ptap = pk / P.Ctot;
+    pch = pk - ptap * P.Ctot;
+    if (P.nsrc > 1 && pch >= P.src[0].C) { pch -= P.src[0].C; ps = 1; }
+  }
+  if (qvec) {
+    qtap = qk / Q.Ctot;
+    qch = qk - qtap * Q.Ctot;
+    if (Q.nsrc > 1 && qch >= Q.src[0].C) { qch -= Q.src[0].C; qs = 1; }
+  }
+  const bool pin = pk < P.K, qin = qk < Q.K;
+
+  uint4 rp[PI], rq[PJ];
+  auto load_stage = [&](int64_t m_base) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int64_t m = m_base + pr + RPI * i;
+      rp[i] = gather_vec8_bf16(P, m < me ? m : P.M, pk, ptap, ps, pch, pvec, pin);
+    }
+#pragma unroll
+    for (int i = 0; i < PJ; ++i) {
+      const int64_t m = m_base + qr + RPJ * i;
+      rq[i] = gather_vec8_bf16(Q, m < me ? m : Q.M, qk, qtap, qs, qch, qvec, qin);
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i) *reinterpret_cast<uint4*>(&Ps[buf][pr + RPI * i][pc * 8]) = rp[i];
+#pragma unroll
+    for (int i = 0; i < PJ; ++i) *reinterpret_cast<uint4*>(&Qs[buf][qr + RPJ * i][qc * 8]) = rq[i];
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  const int64_t nst = (me - mb + KM - 1) / KM;
+  load_stage(mb);
+  store_stage(0);
+  __syncthreads();
+  for (int64_t st = 0; st < nst; ++st) {
+    const int buf = (int)(st & 1);
+    if (st + 1 < nst) load_stage(mb + (st + 1) * KM);
+#pragma unroll
+    for (int ks = 0; ks < KM / 16; ++ks) {
+      const int row = 16 * ks + 8 * half + q4;
+      bf16x8 af[MT], bfr[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) {
+        const int col = wi * WI + a * 32 + 16 * grp_hi + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(&Ps[buf][row][col]));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(&Ps[buf][row + 4][col]));
+        af[a] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const int col = wj * WJ + b * 32 + 16 * grp_hi + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(&Qs[buf][row][col]));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(&Qs[buf][row + 4][col]));
+        bfr[b] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    if (st + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int j = j0 + wj * WJ + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * WI + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
+      }
+    }
+}
+
+// =========================================================================== host side
+static int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems) {
+  SELUNET_REQUIRE(a != nullptr, "gather descriptor is NULL");
+  SELUNET_REQUIRE(a->n > 0 && a->h > 0 && a->w > 0, "gather grid must be positive (%d,%d,%d)", a->n, a->h, a->w);
+  SELUNET_REQUIRE(a->taps == 1 || a->taps == 4 || a->taps == 9, "taps must be 1, 4 or 9 (got %d)", a->taps);
+  SELUNET_REQUIRE(a->nsrc == 1 || a->nsrc == 2, "nsrc must be 1 or 2");
+  std::memset(&g, 0, sizeof(g));
+  g.n = a->n;
+  g.h = a->h;
+  g.w = a->w;
+  g.taps = a->taps;
+  g.nsrc = a->nsrc;
+  g.hs = a->taps == 4 ? 2 * a->h : a->h;
+  g.ws = a->taps == 4 ? 2 * a->w : a->w;
+  g.M = (int64_t)a->n * a->h * a->w;
+  int ctot = 0;
+  bool vec = true;
+  for (int s = 0; s < a->nsrc; ++s) {
+    const selunet_source& src = a->src[s];
+    SELUNET_REQUIRE(src.data != nullptr, "source %d data is NULL", s);
+    SELUNET_REQUIRE(src.channels > 0, "source %d channels must be positive", s);
+    SELUNET_REQUIRE((src.scale == nullptr) == (src.shift == nullptr), "scale/shift must both be set or both NULL");
+    SELUNET_REQUIRE(src.layout == 0 || (src.layout == 1 && a->nsrc == 1 && src.scale == nullptr),
+                    "NCHW (fp32) sources are only supported as a single untransformed source");
+    g.src[s].data = src.data;
+    g.src[s].scale = src.scale;
+    g.src[s].shift = src.shift;
+    g.src[s].C = src.channels;
+    g.src[s].relu = src.relu;
+    g.src[s].layout = src.layout;
+    if (src.channels % vec_elems != 0 || src.layout != 0) vec = false;
+    if ((reinterpret_cast<uintptr_t>(src.data) & 15) != 0) vec = false;
+    ctot += src.channels;
+  }
+  g.Ctot = ctot;
+  g.K = a->taps * ctot;
+  g.small = vec ? 0 : 1;
+  if (g.small) {
+    SELUNET_REQUIRE(a->nsrc == 1 && a->src[0].scale == nullptr,
+                    "element-wise gather (channels %% %d != 0) supports one untransformed source", vec_elems);
+  }
+  return 0;
+}
+
+template <typename T, int BN>
+static void launch_gather(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
+  const int n_tiles = N / BN;
+  const int64_t m_tiles = cdiv(g.M, BM);
+  hipLaunchKernelGGL((gemm_gather_kernel<T, BN>), dim3((unsigned)(m_tiles * n_tiles)), dim3(256), 0, st, g,
+                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles);
+}
+
+template <typename T, int BI, int BJ>
+static void launch_wgrad(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
+                         hipStream_t st) {
+  const int tiles_j = nj_pad / BJ;
+  const int tiles = (ni / BI) * tiles_j;
+  const int64_t M = p.M;
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(2048, tiles)));
+  int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
+  splits = cdiv(M, mchunk);
+  if constexpr (std::is_same<T, float>::value)
+    hipLaunchKernelGGL((gemm_wgrad_kernel<T, BI, BJ>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q, out,
+                       ldo, mchunk, tiles_j, tiles);
+  else
+    hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<BI, BJ>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q,
+                       out, ldo, mchunk, tiles_j, tiles);
+}
+
+}  // namespace selunet
+
+using namespace selunet;
+
+extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
+                                   const selunet_epilogue* ep, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
+  const int esz = dtype == SELUNET_F32 ? 4 : 2;
+  const int bke = 128 / esz;
+  GatherArg g;
+  if (int rc = make_gather(a, dtype, g, 16 / esz)) return rc;
+  SELUNET_REQUIRE(b != nullptr && ep != nullptr && ep->out0 != nullptr, "B / epilogue / out0 must be non-NULL");
+  SELUNET_REQUIRE(n_cols > 0 && n_cols % 64 == 0, "n_cols must be a positive multiple of 64 (got %d)", n_cols);
+  SELUNET_REQUIRE(k_pad >= g.K && k_pad % bke == 0, "k_pad (%d) must be >= K (%d) and a multiple of %d", k_pad, g.K,
+                  bke);
+  SELUNET_REQUIRE(g.small || (g.Ctot % bke == 0 && (a->nsrc == 1 || a->src[0].channels % bke == 0)),
+                  "vector gather needs channel counts that are multiples of %d", bke);
+  SELUNET_REQUIRE(ep->mode >= 0 && ep->mode <= 2, "bad epilogue mode");
+  if (ep->mode == SELUNET_EP_SPLIT)
+    SELUNET_REQUIRE(ep->out1 != nullptr && ep->split > 0 && ep->split < n_cols && ep->split % 64 == 0,
+                    "split epilogue needs out1 and 0 < split < n_cols, split %% 64 == 0");
+  if (ep->mode == SELUNET_EP_SCATTER2X)
+    SELUNET_REQUIRE(n_cols % 4 == 0 && a->taps == 1, "scatter2x epilogue needs taps == 1 and n_cols % 4 == 0");
+  SELUNET_REQUIRE(ep->stats == nullptr || ep->mode == SELUNET_EP_PLAIN, "stats only with the plain epilogue");
+  EpiArg e{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split};
+  hipStream_t st = as_stream(stream);
+  const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
+  if (dtype == SELUNET_F32) {
+    if (bn128) launch_gather<float, 128>(g, b, n_cols, k_pad, e, st);
+    else launch_gather<float, 64>(g, b, n_cols, k_pad, e, st);
+  } else {
+    if (bn128) launch_gather<__bf16, 128>(g, b, n_cols, k_pad, e, st);
+    else launch_gather<__bf16, 64>(g, b, n_cols, k_pad, e, st);
+  }
+  return check_launch("gemm_gather");
+}
+
+extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out, int32_t dtype,
+                                  void* stream) {
+  SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
+  GatherArg gp, gq;
+  const int vec = dtype == SELUNET_F32 ? 4 : 8;  // elements per staged vector
+  if (int rc = make_gather(p, dtype, gp, vec)) return rc;
+  if (int rc = make_gather(q, dtype, gq, vec)) return rc;
+  SELUNET_REQUIRE(out != nullptr, "out is NULL");
+  SELUNET_REQUIRE(gp.M == gq.M && p->n == q->n && p->h == q->h && p->w == q->w, "P and Q must share the row grid");
+  SELUNET_REQUIRE(gp.K % 64 == 0, "P columns (%d) must be a multiple of 64", gp.K);
+  SELUNET_REQUIRE(gp.small == 0, "P must be vector-gatherable");
+  const int ni = gp.K;
+  const int bj = (gq.K % 128 == 0 || gq.K > 512) ? 128 : 64;
+  const int nj_pad = (int)(cdiv(gq.K, bj) * bj);
+  hipStream_t st = as_stream(stream);
+  const bool bi128 = ni % 128 == 0;
+  // out is [ni][nj_pad] where nj_pad = roundup(Kq, 64 or 128): see selunet_wgrad_ld()
+  if (dtype == SELUNET_F32) {
+    if (bi128 && bj == 128) launch_wgrad<float, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else if (bj == 128) launch_wgrad<float, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else if (bi128) launch_wgrad<float, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else launch_wgrad<float, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+  } else {
+    if (bi128 && bj == 128) launch_wgrad<__bf16, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else if (bj == 128) launch_wgrad<__bf16, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else if (bi128) launch_wgrad<__bf16, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    else launch_wgrad<__bf16, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+  }
+  return check_launch("gemm_wgrad");
+}
+
+// leading dimension of the packed wgrad output for a Q operand with kq columns
+extern "C" int32_t selunet_wgrad_ld(int32_t kq) {
+  const int bj = (kq % 128 == 0 || kq > 512) ? 128 : 64;
+  return (int32_t)(cdiv(kq, bj) * bj);
+}

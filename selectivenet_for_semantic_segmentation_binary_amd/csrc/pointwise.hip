@@ -1,0 +1,775 @@
+// Memory-bound kernels of the SelectiveUNet_B step on gfx950: weight (un)packing, deterministic
+// reductions, BatchNorm finalize/backward, MaxPool2d(2), the 1x1 heads, the selective / BCE
+// losses and multi-tensor Adam. All NHWC loads are 4-channel vectors (16 B fp32 / 8 B bf16).
+#include <cstdarg>
+#include <cmath>
+
+#include "common.h"
+
+namespace selunet {
+
+// ------------------------------------------------------------------ error state
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SELUNET_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+  return SELUNET_OK;
+}
+
+constexpr int TPB = 256;
+
+// =========================================================================== packing
+template <typename T>
+__global__ void pack_conv3x3_kernel(const float* __restrict__ w, int co, int ci, int k_pad, T* fwd, T* dgrad) {
+  const int64_t total_f = (int64_t)co * k_pad;
+  const int64_t total_d = dgrad ? (int64_t)ci * 9 * co : 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total_f + total_d;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < total_f) {
+      const int o = (int)(i / k_pad), k = (int)(i % k_pad);
+      float v = 0.0f;
+      if (k < 9 * ci) {
+        const int tap = k / ci, c = k - tap * ci;
+        v = w[((int64_t)o * ci + c) * 9 + tap];
+      }
+      fwd[i] = from_f<T>(v);
+    } else {
+      const int64_t j = i - total_f;
+      const int c = (int)(j / (9 * co));
+      const int k = (int)(j % (9 * co));
+      const int tap = k / co, o = k - tap * co;
+      dgrad[j] = from_f<T>(w[((int64_t)o * ci + c) * 9 + (8 - tap)]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void pack_convT_kernel(const float* __restrict__ w, int ci, int co, T* fwd, T* dgrad) {
+  const int64_t total = (int64_t)ci * co * 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    // w[c][o][ab]
+    const int ab = (int)(i & 3);
+    const int64_t co_ci = i >> 2;
+    const int o = (int)(co_ci % co), c = (int)(co_ci / co);
+    const T v = from_f<T>(w[i]);
+    if (fwd) fwd[((int64_t)ab * co + o) * ci + c] = v;
+    if (dgrad) dgrad[(int64_t)c * 4 * co + ab * co + o] = v;
+  }
+}
+
+__global__ void unpack_conv3x3_kernel(const float* __restrict__ packed, int co, int ci, int ld, float* out) {
+  const int64_t total = (int64_t)co * ci * 9;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % 9);
+    const int64_t oc = i / 9;
+    const int c = (int)(oc % ci), o = (int)(oc / ci);
+    out[i] = packed[(int64_t)o * ld + tap * ci + c];
+  }
+}
+
+__global__ void unpack_convT_kernel(const float* __restrict__ packed, int ci, int co, int ld, float* out) {
+  const int64_t total = (int64_t)ci * co * 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ab = (int)(i & 3);
+    const int64_t r = i >> 2;
+    const int o = (int)(r % co), c = (int)(r / co);
+    out[i] = packed[(int64_t)c * ld + ab * co + o];
+  }
+}
+
+static unsigned grid_for(int64_t n, int64_t cap = 4096) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, TPB), cap));
+}
+
+// =========================================================================== reductions
+constexpr int RED_SPLITS = 128;
+
+__global__ void reduce_rows_l1(const float* __restrict__ slab, int64_t rows, int cols, int64_t chunk, double* ws) {
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;
+  const int64_t r0 = blockIdx.y * chunk;
+  const int64_t r1 = std::min<int64_t>(rows, r0 + chunk);
+  double acc = 0.0;
+  if (col < cols)
+    for (int64_t r = r0 + lane4; r < r1; r += 4) acc += (double)slab[r * cols + col];
+  __shared__ double red[4][64];
+  red[lane4][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (lane4 == 0 && col < cols)
+    ws[(int64_t)blockIdx.y * cols + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void reduce_rows_l2(const double* __restrict__ ws, int splits, int cols, double* out, float* out32) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= cols) return;
+  double acc = 0.0;
+  for (int s = 0; s < splits; ++s) acc += ws[(int64_t)s * cols + col];
+  if (out) out[col] = acc;
+  if (out32) out32[col] = (float)acc;
+}
+
+int64_t channel_slab_rows(int64_t m) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(m, 256), 2048)); }
+
+// Per-channel reduction skeleton over an NHWC [m][C] range: PL pixel lanes x (C/4) channel groups.
+// C in {64,128,256,512}.
+template <typename T, typename F>
+__device__ inline void channel_loop(int64_t m, int C, F&& body) {
+  const int CG = C >> 2;
+  const int PL = TPB / CG;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (m + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk;
+  const int64_t p1 = std::min<int64_t>(m, p0 + chunk);
+  for (int64_t p = p0 + pl; p < p1; p += PL) body(p, cg * 4);
+}
+
+// sum over the PL pixel lanes of a block for NV f32x4 accumulators -> slab row [NV][C]
+template <int NV>
+__device__ inline void channel_block_reduce(f32x4 (&acc)[NV], int C, float* slab_row) {
+  __shared__ f32x4 red[TPB];
+  const int CG = C >> 2;
+  const int PL = TPB / CG;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    red[threadIdx.x] = acc[v];
+    __syncthreads();
+    for (int s = PL / 2; s > 0; s >>= 1) {
+      if (pl < s) red[threadIdx.x] += red[threadIdx.x + s * CG];
+      __syncthreads();
+    }
+    if (pl == 0) *reinterpret_cast<f32x4*>(slab_row + v * C + cg * 4) = red[threadIdx.x];
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ void channel_sum_kernel(const T* __restrict__ x, int64_t m, int C, float* slab) {
+  f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
+  channel_loop<T>(m, C, [&](int64_t p, int c) { acc[0] += Vec4<T>::load(x + p * C + c); });
+  channel_block_reduce<1>(acc, C, slab + (int64_t)blockIdx.x * C);
+}
+
+// =========================================================================== BatchNorm
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t count, int C, const float* conv_bias,
+                                   const float* gamma, const float* beta, float* rmean, float* rvar,
+                                   int64_t* nbt, float momentum, float eps, int training, float* mean_o,
+                                   float* invstd_o, float* scale_o, float* shift_o) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (training && nbt && c == 0) *nbt += 1;
+  if (c >= C) return;
+  const double b = conv_bias ? (double)conv_bias[c] : 0.0;
+  double mean, var;
+  if (training) {
+    mean = sums[c] / (double)count;
+    var = sums[C + c] / (double)count - mean * mean;
+    if (var < 0) var = 0;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * (mean + b));
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * (double)count / (double)(count - 1));
+  } else {
+    mean = (double)rmean[c] - b;  // running stats track conv output *with* bias
+    var = (double)rvar[c];
+  }
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const double sc = (double)gamma[c] * inv;
+  mean_o[c] = (float)mean;
+  invstd_o[c] = (float)inv;
+  scale_o[c] = (float)sc;
+  shift_o[c] = (float)((double)beta[c] - mean * sc);
+}
+
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
+                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                     const float* __restrict__ mean, const float* __restrict__ invstd, float* slab) {
+  f32x4 acc[3] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  const int c0 = (threadIdx.x % (C >> 2)) * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c0);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c0);
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c0);
+  const f32x4 is = *reinterpret_cast<const f32x4*>(invstd + c0);
+  channel_loop<T>(m, C, [&](int64_t p, int c) {
+    const f32x4 yv = Vec4<T>::load(y + p * C + c);
+    const f32x4 g = Vec4<T>::load(dz + p * C + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = yv[e] * sc[e] + sh[e];
+      const float da = z > 0.0f ? g[e] : 0.0f;
+      const float xh = (yv[e] - mu[e]) * is[e];
+      acc[0][e] += da;
+      acc[1][e] += da * xh;
+      acc[2][e] += xh;
+    }
+  });
+  channel_block_reduce<3>(acc, C, slab + (int64_t)blockIdx.x * 3 * C);
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int64_t count, int C, const float* gamma,
+                                       const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sda = sums[c], sdax = sums[C + c], sx = sums[2 * C + c];
+  const double k0 = (double)gamma[c] * invstd[c];
+  const double k1 = k0 * sda / (double)count;
+  const double k2 = k0 * sdax / (double)count;
+  if (dgamma) dgamma[c] = (float)sdax;
+  if (dbeta) dbeta[c] = (float)sda;
+  // sum over pixels of the conv-output gradient; analytically zero (BN removes the mean)
+  if (dbias) dbias[c] = (float)(k0 * sda - (double)count * k1 - k2 * sx);
+  coef[c] = (float)k0;
+  coef[C + c] = (float)k1;
+  coef[2 * C + c] = (float)k2;
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
+                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                    const float* __restrict__ coef, T* __restrict__ dy) {
+  const int64_t nv = m * C / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i * 4) % C);
+    const f32x4 yv = Vec4<T>::load(y + i * 4);
+    const f32x4 g = Vec4<T>::load(dz + i * 4);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = yv[e] * scale[c + e] + shift[c + e];
+      const float da = z > 0.0f ? g[e] : 0.0f;
+      const float xh = (yv[e] - mean[c + e]) * invstd[c + e];
+      o[e] = coef[c + e] * da - coef[C + c + e] - coef[2 * C + c + e] * xh;
+    }
+    Vec4<T>::store(dy + i * 4, o);
+  }
+}
+
+// =========================================================================== MaxPool2d(2)
+template <typename T>
+__device__ inline f32x4 bn_relu4(const T* p, const float* scale, const float* shift, int c) {
+  f32x4 v = Vec4<T>::load(p);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * scale[c + e] + shift[c + e], 0.0f);
+  return v;
+}
+
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ y, int n, int h, int w, int C, const float* scale,
+                                   const float* shift, T* __restrict__ out) {
+  const int ho = h >> 1, wo = w >> 1;
+  const int64_t nv = (int64_t)n * ho * wo * (C / 4);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (C / 4)) * 4;
+    int64_t p = i / (C / 4);
+    const int xo = (int)(p % wo);
+    p /= wo;
+    const int yo = (int)(p % ho);
+    const int64_t img = p / ho;
+    const T* b = y + ((img * h + 2 * yo) * w + 2 * xo) * C + c;
+    f32x4 best = bn_relu4(b, scale, shift, c);
+    const f32x4 v1 = bn_relu4(b + C, scale, shift, c);
+    const f32x4 v2 = bn_relu4(b + (int64_t)w * C, scale, shift, c);
+    const f32x4 v3 = bn_relu4(b + (int64_t)w * C + C, scale, shift, c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (v1[e] > best[e]) best[e] = v1[e];
+      if (v2[e] > best[e]) best[e] = v2[e];
+      if (v3[e] > best[e]) best[e] = v3[e];
+    }
+    Vec4<T>::store(out + i * 4, best);
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w, int C, const float* scale,
+                                   const float* shift, const T* __restrict__ dp, const T* __restrict__ dskip,
+                                   T* __restrict__ dz) {
+  const int ho = h >> 1, wo = w >> 1;
+  const int64_t nv = (int64_t)n * ho * wo * (C / 4);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (C / 4)) * 4;
+    int64_t p = i / (C / 4);
+    const int xo = (int)(p % wo);
+    p /= wo;
+    const int yo = (int)(p % ho);
+    const int64_t img = p / ho;
+    const int64_t off[4] = {((img * h + 2 * yo) * w + 2 * xo) * C + c, ((img * h + 2 * yo) * w + 2 * xo + 1) * C + c,
+                            ((img * h + 2 * yo + 1) * w + 2 * xo) * C + c,
+                            ((img * h + 2 * yo + 1) * w + 2 * xo + 1) * C + c};
+    f32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = bn_relu4(y + off[q], scale, shift, c);
+    int arg[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float best = v[0][e];
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (v[q][e] > best) {  // first maximum in row-major window order (ATen, strict >)
+          best = v[q][e];
+          arg[e] = q;
+        }
+    }
+    const f32x4 g = Vec4<T>::load(dp + i * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 o = dskip ? Vec4<T>::load(dskip + off[q]) : f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (arg[e] == q) o[e] += g[e];
+      Vec4<T>::store(dz + off[q], o);
+    }
+  }
+}
+
+// =========================================================================== 1x1 heads (C = 64)
+// 16 lanes per pixel, 4 channels per lane; 4 pixels per wave instruction.
+template <typename T>
+__global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                 const float* __restrict__ shift, const float* __restrict__ w,
+                                 const float* __restrict__ b, int nh, float* o0, float* o1, float* o2) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+  f32x4 wv[3];
+  for (int h = 0; h < 3; ++h) wv[h] = h < nh ? *reinterpret_cast<const f32x4*>(w + h * 64 + c) : f32x4{0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 4);
+  for (int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4); p < m; p += stride) {
+    f32x4 z = Vec4<T>::load(y + p * 64 + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = fmaxf(z[e] * sc[e] + sh[e], 0.0f);
+    float acc[3];
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      float a = z[0] * wv[h][0] + z[1] * wv[h][1] + z[2] * wv[h][2] + z[3] * wv[h][3];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 16);
+      acc[h] = a;
+    }
+    if (sub == 0) {
+      o0[p] = acc[0] + b[0];
+      if (nh > 1) {
+        o1[p] = acc[1] + b[1];
+        o2[p] = acc[2] + b[2];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                 const float* __restrict__ shift, const float* __restrict__ w, int nh,
+                                 const float* __restrict__ g0, const float* __restrict__ g1,
+                                 const float* __restrict__ g2, T* __restrict__ dz, float* slab) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+  f32x4 wv[3];
+  for (int h = 0; h < 3; ++h) wv[h] = h < nh ? *reinterpret_cast<const f32x4*>(w + h * 64 + c) : f32x4{0, 0, 0, 0};
+  f32x4 dw[3] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  float db[3] = {0, 0, 0};
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (m + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(m, p0 + chunk);
+  for (int64_t p = p0 + (threadIdx.x >> 4); p < p1; p += (TPB >> 4)) {
+    f32x4 z = Vec4<T>::load(y + p * 64 + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = fmaxf(z[e] * sc[e] + sh[e], 0.0f);
+    float g[3] = {g0[p], nh > 1 ? g1[p] : 0.0f, nh > 1 ? g2[p] : 0.0f};
+    f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];
+    Vec4<T>::store(dz + p * 64 + c, d);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      dw[h] += z * g[h];
+      db[h] += g[h];
+    }
+  }
+  // block reduce: 16 pixel lanes per channel group
+  __shared__ float red[TPB][13];
+  for (int h = 0; h < 3; ++h) {
+    red[threadIdx.x][h * 4 + 0] = dw[h][0];
+    red[threadIdx.x][h * 4 + 1] = dw[h][1];
+    red[threadIdx.x][h * 4 + 2] = dw[h][2];
+    red[threadIdx.x][h * 4 + 3] = dw[h][3];
+  }
+  __syncthreads();
+  float* row = slab + (int64_t)blockIdx.x * nh * 65;
+  if (threadIdx.x < 16) {
+    for (int h = 0; h < nh; ++h)
+      for (int e = 0; e < 4; ++e) {
+        float s = 0.0f;
+        for (int q = 0; q < 16; ++q) s += red[q * 16 + threadIdx.x][h * 4 + e];
+        row[h * 65 + threadIdx.x * 4 + e] = s;
+      }
+  }
+  __syncthreads();
+  // bias: each pixel is seen by 16 lanes; the sub == 0 lane carries its g
+  for (int h = 0; h < nh; ++h) {
+    red[threadIdx.x][12] = (sub == 0) ? db[h] : 0.0f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.0f;
+      for (int q = 0; q < TPB; q += 16) s += red[q][12];
+      row[h * 65 + 64] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// =========================================================================== losses
+int64_t loss_slab_rows(int64_t p) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(p, 4096), 1024)); }
+
+template <int NV>
+__device__ inline void block_sum_store(float (&v)[NV], float* dst) {
+  __shared__ float red[NV][TPB / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float s = wave_sum(v[k]);
+    if (lane == 0) red[k][wv] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    float s = 0.0f;
+    for (int q = 0; q < TPB / 64; ++q) s += red[threadIdx.x][q];
+    dst[threadIdx.x] = s;
+  }
+}
+
+__global__ void selective_partials_kernel(const float* __restrict__ out, const float* __restrict__ sel,
+                                          const float* __restrict__ tgt, int64_t P, float* slab) {
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (P + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(P, p0 + chunk);
+  float acc[2] = {0.0f, 0.0f};
+  for (int64_t i = p0 + threadIdx.x; i < p1; i += TPB) {
+    const float s = sigmoidf_(sel[i]);
+    const float x = out[i], t = tgt[i];
+    const float ell = t * softplusf_(-x) + (1.0f - t) * softplusf_(x);
+    acc[0] += s;
+    acc[1] += ell * s;
+  }
+  block_sum_store<2>(acc, slab + blockIdx.x * 2);
+}
+
+__global__ void selective_finalize_kernel(const double* sums, double P, float lamb, float tc, float* loss,
+                                          float* coverage, float* state) {
+  const double S0 = sums[0], S1 = sums[1];
+  const double cov = S0 / P;
+  const double R = S1 / S0;
+  const double d = fmax((double)tc - cov, 0.0);
+  loss[0] = (float)(R + (double)lamb * d * d);
+  coverage[0] = (float)cov;
+  state[0] = (float)S0;
+  state[1] = (float)R;
+  state[2] = (float)d;
+  state[3] = (float)P;
+}
+
+__global__ void selective_bwd_kernel(const float* __restrict__ out, const float* __restrict__ sel,
+                                     const float* __restrict__ tgt, int64_t P, const float* state, float lamb,
+                                     const float* g_loss, const float* g_cov, float* d_out, float* d_sel) {
+  const float S0 = state[0], R = state[1], d = state[2], Pg = state[3];
+  const float gl = g_loss ? g_loss[0] : 1.0f;
+  const float gc = g_cov ? g_cov[0] : 0.0f;
+  const float inv_s0 = 1.0f / S0;
+  const float cterm = (gc - gl * 2.0f * lamb * d) / Pg;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const float s = sigmoidf_(sel[i]);
+    const float x = out[i], t = tgt[i];
+    const float px = sigmoidf_(x);
+    const float ell = t * softplusf_(-x) + (1.0f - t) * softplusf_(x);
+    d_out[i] = gl * s * (px - t) * inv_s0;
+    d_sel[i] = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
+  }
+}
+
+__global__ void bce_partials_kernel(const float* __restrict__ a, const float* __restrict__ t, int64_t P, float* slab) {
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (P + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(P, p0 + chunk);
+  float acc[1] = {0.0f};
+  for (int64_t i = p0 + threadIdx.x; i < p1; i += TPB) {
+    const float x = a[i], y = t[i];
+    acc[0] += (1.0f - y) * x + softplusf_(-x);  // = -[y log s(x) + (1-y) log(1-s(x))]
+  }
+  block_sum_store<1>(acc, slab + blockIdx.x);
+}
+
+__global__ void bce_finalize_kernel(const double* sums, double P, float* loss) { loss[0] = (float)(sums[0] / P); }
+
+__global__ void bce_bwd_kernel(const float* __restrict__ a, const float* __restrict__ t, int64_t P, float inv_p,
+                               const float* g_loss, float* d) {
+  const float g = g_loss ? g_loss[0] : 1.0f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = g * (sigmoidf_(a[i]) - t[i]) * inv_p;
+}
+
+// =========================================================================== Adam
+__global__ void adam_kernel(const selunet_adam_tensor* __restrict__ list, int n, float lr_bc1, float beta1,
+                            float beta2, float eps, float wd, float bc2_sqrt) {
+  const int64_t chunk = blockIdx.x;
+  int t = 0;
+  while (t + 1 < n && list[t + 1].chunk_begin <= chunk) ++t;
+  const selunet_adam_tensor T = list[t];
+  const int64_t base = (chunk - T.chunk_begin) * SELUNET_ADAM_CHUNK;
+  const int64_t end = std::min<int64_t>(T.numel, base + SELUNET_ADAM_CHUNK);
+  for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
+    float g = T.grad[i];
+    float p = T.param[i];
+    if (wd != 0.0f) g += wd * p;
+    float m = T.exp_avg[i];
+    m = m + (1.0f - beta1) * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
+    float v = T.exp_avg_sq[i] * beta2 + (1.0f - beta2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p - lr_bc1 * (m / denom);
+    T.exp_avg[i] = m;
+    T.exp_avg_sq[i] = v;
+    T.param[i] = p;
+  }
+}
+
+}  // namespace selunet
+
+using namespace selunet;
+
+#define DISPATCH_T(dtype, ...)                                                      \
+  do {                                                                              \
+    if ((dtype) == SELUNET_F32) {                                                   \
+      using T = float;                                                              \
+      __VA_ARGS__;                                                                  \
+    } else if ((dtype) == SELUNET_BF16) {                                           \
+      using T = __bf16;                                                             \
+      __VA_ARGS__;                                                                  \
+    } else {                                                                        \
+      return fail(SELUNET_EINVAL, "dtype must be SELUNET_F32 or SELUNET_BF16");    \
+    }                                                                               \
+  } while (0)
+
+static bool ok_channels(int32_t c) { return c == 64 || c == 128 || c == 256 || c == 512; }
+
+extern "C" {
+
+const char* selunet_last_error(void) { return g_err; }
+int32_t selunet_version(void) { return 1; }
+
+int selunet_pack_conv3x3(const float* w, int32_t co, int32_t ci, int32_t k_pad, void* fwd, void* dgrad,
+                         int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(w && fwd && co > 0 && ci > 0 && k_pad >= 9 * ci, "pack_conv3x3: bad arguments");
+  const int64_t total = (int64_t)co * k_pad + (dgrad ? (int64_t)ci * 9 * co : 0);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_conv3x3_kernel<T>, dim3(grid_for(total)), dim3(TPB), 0, as_stream(stream),
+                                       w, co, ci, k_pad, (T*)fwd, (T*)dgrad));
+  return check_launch("pack_conv3x3");
+}
+
+int selunet_pack_convT(const float* w, int32_t ci, int32_t co, void* fwd, void* dgrad, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(w && (fwd || dgrad) && co > 0 && ci > 0, "pack_convT: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_convT_kernel<T>, dim3(grid_for((int64_t)ci * co * 4)), dim3(TPB), 0,
+                                       as_stream(stream), w, ci, co, (T*)fwd, (T*)dgrad));
+  return check_launch("pack_convT");
+}
+
+int selunet_unpack_conv3x3_grad(const float* packed, int32_t co, int32_t ci, int32_t ld, float* out, void* stream) {
+  SELUNET_REQUIRE(packed && out && co > 0 && ci > 0 && ld >= 9 * ci, "unpack_conv3x3_grad: bad arguments");
+  hipLaunchKernelGGL(unpack_conv3x3_kernel, dim3(grid_for((int64_t)co * ci * 9)), dim3(TPB), 0, as_stream(stream),
+                     packed, co, ci, ld, out);
+  return check_launch("unpack_conv3x3_grad");
+}
+
+int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float* out, void* stream) {
+  SELUNET_REQUIRE(packed && out && co > 0 && ci > 0, "unpack_convT_grad: bad arguments");
+  const int ld = selunet_wgrad_ld(4 * co);
+  hipLaunchKernelGGL(unpack_convT_kernel, dim3(grid_for((int64_t)co * ci * 4)), dim3(TPB), 0, as_stream(stream),
+                     packed, ci, co, ld, out);
+  return check_launch("unpack_convT_grad");
+}
+
+int64_t selunet_reduce_ws_bytes(int32_t cols) { return (int64_t)RED_SPLITS * cols * (int64_t)sizeof(double); }
+
+int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* ws, double* out, float* out32,
+                        void* stream) {
+  SELUNET_REQUIRE(slab && ws && (out || out32) && rows > 0 && cols > 0, "reduce_rows: bad arguments");
+  const int splits = (int)std::min<int64_t>(RED_SPLITS, cdiv(rows, 16));
+  const int64_t chunk = cdiv(rows, splits);
+  hipLaunchKernelGGL(reduce_rows_l1, dim3((unsigned)cdiv(cols, 64), splits), dim3(TPB), 0, as_stream(stream), slab,
+                     rows, cols, chunk, ws);
+  hipLaunchKernelGGL(reduce_rows_l2, dim3((unsigned)cdiv(cols, TPB)), dim3(TPB), 0, as_stream(stream), ws, splits,
+                     cols, out, out32);
+  return check_launch("reduce_rows");
+}
+
+int64_t selunet_channel_slab_rows(int64_t m) { return channel_slab_rows(m); }
+
+int selunet_channel_sum(const void* x, int64_t m, int32_t c, float* slab, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(x && slab && m > 0 && ok_channels(c), "channel_sum: bad arguments (C=%d)", c);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(channel_sum_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)x, m, c, slab));
+  return check_launch("channel_sum");
+}
+
+int selunet_bn_finalize(const double* sums, int64_t count, int32_t c, const float* conv_bias, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
+                        float momentum, float eps, int32_t training, float* mean, float* invstd, float* scale,
+                        float* shift, void* stream) {
+  SELUNET_REQUIRE(gamma && beta && mean && invstd && scale && shift && c > 0, "bn_finalize: bad arguments");
+  if (training) {
+    SELUNET_REQUIRE(sums != nullptr, "bn_finalize: sums is NULL");
+    SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
+  } else {
+    SELUNET_REQUIRE(running_mean && running_var, "bn_finalize(eval): running stats are NULL");
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums, count,
+                     c, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, mean,
+                     invstd, scale, shift);
+  return check_launch("bn_finalize");
+}
+
+int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, const float* scale, const float* shift,
+                          const float* mean, const float* invstd, float* slab, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && slab && m > 0 && ok_channels(c),
+                  "bn_bwd_reduce: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd,
+                                       slab));
+  return check_launch("bn_bwd_reduce");
+}
+
+int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const float* gamma, const float* invstd,
+                            float* dgamma, float* dbeta, float* dbias, float* coef, void* stream) {
+  SELUNET_REQUIRE(sums && gamma && invstd && coef && c > 0 && count > 0, "bn_bwd_finalize: bad arguments");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums,
+                     count, c, gamma, invstd, dgamma, dbeta, dbias, coef);
+  return check_launch("bn_bwd_finalize");
+}
+
+int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, const float* coef, void* dy, int32_t dtype,
+                         void* stream) {
+  SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
+                  "bn_bwd_apply: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(m * c / 4, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd,
+                                       coef, (T*)dy));
+  return check_launch("bn_bwd_apply");
+}
+
+int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,
+                         const float* shift, void* out, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && out && scale && shift && n > 0 && h > 1 && w > 1 && c % 4 == 0, "maxpool2_fwd: bad arguments");
+  SELUNET_REQUIRE(h % 2 == 0 && w % 2 == 0, "maxpool2_fwd: H and W must be even (got %d x %d)", h, w);
+  const int64_t nv = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(nv, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, n, h, w, c, scale, shift, (T*)out));
+  return check_launch("maxpool2_fwd");
+}
+
+int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,
+                         const float* shift, const void* dpool, const void* dskip, void* dz, int32_t dtype,
+                         void* stream) {
+  SELUNET_REQUIRE(y && dpool && dz && scale && shift && n > 0 && h % 2 == 0 && w % 2 == 0 && c % 4 == 0,
+                  "maxpool2_bwd: bad arguments");
+  const int64_t nv = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(nv, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, n, h, w, c, scale, shift, (const T*)dpool,
+                                       (const T*)dskip, (T*)dz));
+  return check_launch("maxpool2_bwd");
+}
+
+int selunet_heads_fwd(const void* y, int64_t m, const float* scale, const float* shift, const float* w,
+                      const float* b, int32_t nh, float* out0, float* out1, float* out2, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && w && b && out0 && m > 0 && (nh == 1 || nh == 3), "heads_fwd: bad arguments");
+  SELUNET_REQUIRE(nh == 1 || (out1 && out2), "heads_fwd: out1/out2 required for 3 heads");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(heads_fwd_kernel<T>, dim3(grid_for(m * 16, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, w, b, nh, out0, out1, out2));
+  return check_launch("heads_fwd");
+}
+
+int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float* shift, const float* w, int32_t nh,
+                      const float* g0, const float* g1, const float* g2, void* dz, float* slab, int32_t dtype,
+                      void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && w && g0 && dz && slab && m > 0 && (nh == 1 || nh == 3),
+                  "heads_bwd: bad arguments");
+  SELUNET_REQUIRE(nh == 1 || (g1 && g2), "heads_bwd: g1/g2 required for 3 heads");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(heads_bwd_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, w, nh, g0, g1, g2, (T*)dz,
+                                       slab));
+  return check_launch("heads_bwd");
+}
+
+int64_t selunet_loss_slab_rows(int64_t p) { return loss_slab_rows(p); }
+
+int selunet_selective_partials(const float* out, const float* sel, const float* target, int64_t p, float* slab,
+                               void* stream) {
+  SELUNET_REQUIRE(out && sel && target && slab && p > 0, "selective_partials: bad arguments");
+  hipLaunchKernelGGL(selective_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream),
+                     out, sel, target, p, slab);
+  return check_launch("selective_partials");
+}
+
+int selunet_selective_finalize(const double* sums, double p_global, float lamb, float target_coverage, float* loss,
+                               float* coverage, float* state, void* stream) {
+  SELUNET_REQUIRE(sums && loss && coverage && state && p_global > 0, "selective_finalize: bad arguments");
+  hipLaunchKernelGGL(selective_finalize_kernel, dim3(1), dim3(1), 0, as_stream(stream), sums, p_global, lamb,
+                     target_coverage, loss, coverage, state);
+  return check_launch("selective_finalize");
+}
+
+int selunet_selective_bwd(const float* out, const float* sel, const float* target, int64_t p, const float* state,
+                          float lamb, const float* g_loss, const float* g_coverage, float* d_out, float* d_sel,
+                          void* stream) {
+  SELUNET_REQUIRE(out && sel && target && state && d_out && d_sel && p > 0, "selective_bwd: bad arguments");
+  hipLaunchKernelGGL(selective_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), out, sel, target,
+                     p, state, lamb, g_loss, g_coverage, d_out, d_sel);
+  return check_launch("selective_bwd");
+}
+
+int selunet_bce_partials(const float* logit, const float* target, int64_t p, float* slab, void* stream) {
+  SELUNET_REQUIRE(logit && target && slab && p > 0, "bce_partials: bad arguments");
+  hipLaunchKernelGGL(bce_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream), logit,
+                     target, p, slab);
+  return check_launch("bce_partials");
+}
+
+int selunet_bce_finalize(const double* sums, double p_global, float* loss, void* stream) {
+  SELUNET_REQUIRE(sums && loss && p_global > 0, "bce_finalize: bad arguments");
+  hipLaunchKernelGGL(bce_finalize_kernel, dim3(1), dim3(1), 0, as_stream(stream), sums, p_global, loss);
+  return check_launch("bce_finalize");
+}
+
+int selunet_bce_bwd(const float* logit, const float* target, int64_t p, double p_global, const float* g_loss,
+                    float* d_logit, void* stream) {
+  SELUNET_REQUIRE(logit && target && d_logit && p > 0 && p_global > 0, "bce_bwd: bad arguments");
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), logit, target, p,
+                     (float)(1.0 / p_global), g_loss, d_logit);
+  return check_launch("bce_bwd");
+}
+
+int selunet_adam_step(const selunet_adam_tensor* list, int32_t n, int64_t total_chunks, float lr, float beta1,
+                      float beta2, float eps, float weight_decay, int64_t step, void* stream) {
+  SELUNET_REQUIRE(list && n > 0 && total_chunks > 0 && step > 0, "adam_step: bad arguments");
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)total_chunks), dim3(TPB), 0, as_stream(stream), list, n,
+                     (float)(lr / bc1), beta1, beta2, eps, weight_decay, (float)std::sqrt(bc2));
+  return check_launch("adam_step");
+}
+
+}  // extern "C"

@@ -1,0 +1,304 @@
+"""Kernel sequencing for one UNet_B forward / backward on the MI355X (no autograd inside).
+
+This is the host side of the hot path: it mirrors `UNet_B.forward` (model.py:68-103) layer by
+layer, but every op is a call into libselunet.so. Layout in HBM: activations NHWC, element
+type `dt` (fp32 for the parity configuration, bf16 for the fast one); per-layer state kept for
+the backward is only the pre-BN conv output `y` (its BN+ReLU is re-applied by whichever kernel
+reads it), the folded BN scale/shift/mean/invstd, the 3 pooled tensors and the 3 up-sampled
+tensors — `torch.cat` is never materialised (the decoder GEMMs read two sources).
+
+Backward order (train.py:208 autograd, restated explicitly):
+heads -> dec1_1 -> dec1_2 (dgrad split into d(up1), d(skip1)) -> unpool1 -> dec2_1 -> ... ->
+bottleneck -> pool3 backward (+ d(skip3)) -> enc3_2 -> ... -> enc1_1 (no data gradient).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as K
+from . import layout as LY
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def _rup(a, b):
+    return (a + b - 1) // b * b
+
+
+@dataclass
+class BNState:
+    y: torch.Tensor          # pre-BN conv output (no bias), NHWC [M][C]
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+    n: int
+    h: int
+    w: int
+    c: int
+
+    def src(self):
+        return K.source(self.y, self.c, self.scale, self.shift, relu=True)
+
+
+@dataclass
+class Ctx:
+    dt: torch.dtype
+    training: bool
+    selective: bool
+    shape: tuple
+    x: torch.Tensor = None
+    bn: dict = field(default_factory=dict)
+    pools: dict = field(default_factory=dict)
+    ups: dict = field(default_factory=dict)
+    wpack: dict = field(default_factory=dict)
+
+
+class Engine:
+    """Stateless sequencer; parameters/buffers are passed in as dicts of tensors."""
+
+    def __init__(self, dt: torch.dtype = torch.float32):
+        self.dt = dt
+        self.code = K.dtype_code(dt)
+        self.bke = 128 // torch.empty((), dtype=dt).element_size()
+
+    # ------------------------------------------------------------------ small helpers
+    def _reduce(self, slab, rows, cols, out64=None, out32=None):
+        ws = torch.empty(K.query("selunet_reduce_ws_bytes", cols) // 8, dtype=torch.float64, device=slab.device)
+        K.call("selunet_reduce_rows", K.ptr(slab), rows, cols, K.ptr(ws), K.ptr(out64), K.ptr(out32), self.stream)
+
+    @property
+    def stream(self):
+        return K.stream_ptr()
+
+    def pack_weights(self, P, need_dgrad=True):
+        """fp32 master weights -> GEMM operand layouts in the compute dtype."""
+        dev = P["encoder_layer_1_2.0.weight"].device
+        packs = {}
+        for name, ci, co in LY.CBR_LAYERS:
+            w = P[f"{name}.0.weight"]
+            ci = w.shape[1]
+            kpad = _rup(9 * ci, self.bke)
+            fwd = torch.empty(co, kpad, dtype=self.dt, device=dev)
+            dg = None
+            if need_dgrad and name != "encoder_layer_1_1":
+                dg = torch.empty(ci, 9 * co, dtype=self.dt, device=dev)
+            K.call("selunet_pack_conv3x3", K.ptr(w), co, ci, kpad, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
+            packs[name] = (fwd, dg, kpad)
+        for name, ci, co in LY.UNPOOLS:
+            w = P[f"{name}.weight"]
+            fwd = torch.empty(4 * co, ci, dtype=self.dt, device=dev)
+            dg = torch.empty(ci, 4 * co, dtype=self.dt, device=dev) if need_dgrad else None
+            K.call("selunet_pack_convT", K.ptr(w), ci, co, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
+            packs[name] = (fwd, dg, ci)
+        return packs
+
+    # ------------------------------------------------------------------ forward pieces
+    def _cbr(self, ctx, name, P, B, n, h, w, *srcs):
+        fwd, _, kpad = ctx.wpack[name]
+        co = fwd.shape[0]
+        M = n * h * w
+        dev = fwd.device
+        y = torch.empty(M, co, dtype=self.dt, device=dev)
+        stats = None
+        rows = (M + K.GEMM_BM - 1) // K.GEMM_BM
+        if ctx.training:
+            stats = torch.empty(rows, 2, co, dtype=torch.float32, device=dev)
+        g = K.gather(n, h, w, 9, *srcs)
+        ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+        K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
+        mean, invstd, scale, shift = (torch.empty(co, dtype=torch.float32, device=dev) for _ in range(4))
+        sums = None
+        if ctx.training:
+            sums = torch.empty(2 * co, dtype=torch.float64, device=dev)
+            self._reduce(stats, rows, 2 * co, out64=sums)
+        K.call("selunet_bn_finalize", K.ptr(sums), M, co, K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]),
+               K.ptr(P[f"{name}.1.bias"]), K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
+               K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, int(ctx.training),
+               K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+        st = BNState(y, mean, invstd, scale, shift, n, h, w, co)
+        ctx.bn[name] = st
+        return st
+
+    def _pool(self, ctx, key, st: BNState):
+        out = torch.empty(st.n * (st.h // 2) * (st.w // 2), st.c, dtype=self.dt, device=st.y.device)
+        K.call("selunet_maxpool2_fwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
+               K.ptr(out), self.code, self.stream)
+        ctx.pools[key] = out
+        return out
+
+    def _up(self, ctx, name, P, st: BNState):
+        fwd, _, ci = ctx.wpack[name]
+        co = fwd.shape[0] // 4
+        out = torch.empty(st.n * 2 * st.h * 2 * st.w, co, dtype=self.dt, device=st.y.device)
+        g = K.gather(st.n, st.h, st.w, 1, st.src())
+        ep = K.Epilogue(K.ptr(out), None, K.ptr(P[f"{name}.bias"]), None, K.EP_SCATTER2X, 0)
+        K.call("selunet_gemm_gather", g, K.ptr(fwd), 4 * co, ci, ep, self.code, self.stream)
+        ctx.ups[name] = out
+        return out
+
+    def forward(self, x, P, B, selective, training, need_backward=False):
+        """x: [N, Cin, H, W] fp32 contiguous. Returns (heads tuple, ctx)."""
+        assert x.dim() == 4 and x.is_contiguous() and x.dtype == torch.float32
+        n, cin, H, W = x.shape
+        if H % 8 or W % 8:
+            raise ValueError(f"UNet_B needs H and W divisible by 8 (three 2x2 poolings); got {H}x{W}")
+        ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
+        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
+        c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
+        h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
+        e11 = c("encoder_layer_1_1", h1, w1, K.source(x, cin, layout=1))
+        e12 = c("encoder_layer_1_2", h1, w1, e11.src())
+        p1 = self._pool(ctx, "pool1", e12)
+        e21 = c("encoder_layer_2_1", h2, w2, K.source(p1, 64))
+        e22 = c("encoder_layer_2_2", h2, w2, e21.src())
+        p2 = self._pool(ctx, "pool2", e22)
+        e31 = c("encoder_layer_3_1", h3, w3, K.source(p2, 128))
+        e32 = c("encoder_layer_3_2", h3, w3, e31.src())
+        p3 = self._pool(ctx, "pool3", e32)
+        b42 = c("decoder_layer_4_2", h4, w4, K.source(p3, 256))
+        b41 = c("decoder_layer_4_1", h4, w4, b42.src())
+        u3 = self._up(ctx, "unpool3", P, b41)
+        d32 = c("decoder_layer_3_2", h3, w3, K.source(u3, 256), e32.src())
+        d31 = c("decoder_layer_3_1", h3, w3, d32.src())
+        u2 = self._up(ctx, "unpool2", P, d31)
+        d22 = c("decoder_layer_2_2", h2, w2, K.source(u2, 128), e22.src())
+        d21 = c("decoder_layer_2_1", h2, w2, d22.src())
+        u1 = self._up(ctx, "unpool1", P, d21)
+        d12 = c("decoder_layer_1_2", h1, w1, K.source(u1, 64), e12.src())
+        d11 = c("decoder_layer_1_1", h1, w1, d12.src())
+        M = n * H * W
+        heads = LY.HEADS if selective else LY.HEADS[:1]
+        hw = torch.cat([P[f"{h}.weight"].reshape(1, 64) for h in heads]).contiguous()
+        hb = torch.cat([P[f"{h}.bias"].reshape(1) for h in heads]).contiguous()
+        outs = [torch.empty(n, H, W, dtype=torch.float32, device=x.device) for _ in heads]
+        o = outs + [None] * (3 - len(outs))
+        K.call("selunet_heads_fwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(hw), K.ptr(hb),
+               len(heads), K.ptr(o[0]), K.ptr(o[1]), K.ptr(o[2]), self.code, self.stream)
+        ctx.head_w = hw
+        return tuple(outs), ctx
+
+    # ------------------------------------------------------------------ backward pieces
+    def _cbr_bwd(self, ctx, name, dz, G, input_srcs, dgrad_split=None, need_dgrad=True):
+        """BN+ReLU backward then conv weight/bias grads; returns the data gradient (or split pair)."""
+        st: BNState = ctx.bn[name]
+        M, co, dev = st.n * st.h * st.w, st.c, st.y.device
+        rows = K.query("selunet_channel_slab_rows", M)
+        slab = torch.empty(rows, 3, co, dtype=torch.float32, device=dev)
+        K.call("selunet_bn_bwd_reduce", K.ptr(dz), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+               K.ptr(st.mean), K.ptr(st.invstd), K.ptr(slab), self.code, self.stream)
+        sums = torch.empty(3 * co, dtype=torch.float64, device=dev)
+        self._reduce(slab, rows, 3 * co, out64=sums)
+        coef = torch.empty(3, co, dtype=torch.float32, device=dev)
+        gamma = ctx.params[f"{name}.1.weight"]
+        K.call("selunet_bn_bwd_finalize", K.ptr(sums), M, co, K.ptr(gamma), K.ptr(st.invstd),
+               K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]), K.ptr(coef),
+               self.stream)
+        dy = torch.empty(M, co, dtype=self.dt, device=dev)
+        K.call("selunet_bn_bwd_apply", K.ptr(dz), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+               K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
+        # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
+        ci = sum(s.channels for s in input_srcs)
+        ld = K.query("selunet_wgrad_ld", 9 * ci)
+        packed = torch.zeros(co, ld, dtype=torch.float32, device=dev)
+        gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
+        gq = K.gather(st.n, st.h, st.w, 9, *input_srcs)
+        K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
+        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
+        if not need_dgrad:
+            return None
+        _, wd, _ = ctx.wpack[name]
+        ga = K.gather(st.n, st.h, st.w, 9, K.source(dy, co))
+        if dgrad_split is None:
+            dx = torch.empty(M, ci, dtype=self.dt, device=dev)
+            ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+            K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
+            return dx
+        c0 = dgrad_split
+        d0 = torch.empty(M, c0, dtype=self.dt, device=dev)
+        d1 = torch.empty(M, ci - c0, dtype=self.dt, device=dev)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0)
+        K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
+        return d0, d1
+
+    def _up_bwd(self, ctx, name, du, G, prev: BNState):
+        """ConvTranspose2d(k2,s2) backward: bias/weight grads and the data gradient."""
+        fwd, wd, ci = ctx.wpack[name]
+        co = fwd.shape[0] // 4
+        n, h, w = prev.n, prev.h, prev.w
+        dev = du.device
+        Mu = n * 4 * h * w
+        rows = K.query("selunet_channel_slab_rows", Mu)
+        slab = torch.empty(rows, co, dtype=torch.float32, device=dev)
+        K.call("selunet_channel_sum", K.ptr(du), Mu, co, K.ptr(slab), self.code, self.stream)
+        self._reduce(slab, rows, co, out32=G[f"{name}.bias"])
+        ld = K.query("selunet_wgrad_ld", 4 * co)
+        packed = torch.zeros(ci, ld, dtype=torch.float32, device=dev)
+        gp = K.gather(n, h, w, 1, prev.src())
+        gq = K.gather(n, h, w, 4, K.source(du, co))
+        K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
+        K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
+        dz = torch.empty(n * h * w, ci, dtype=self.dt, device=dev)
+        ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
+        K.call("selunet_gemm_gather", K.gather(n, h, w, 4, K.source(du, co)), K.ptr(wd), ci, 4 * co, ep, self.code,
+               self.stream)
+        return dz
+
+    def _pool_bwd(self, st: BNState, dp, dskip):
+        dz = torch.empty_like(st.y)
+        K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
+               K.ptr(dp), K.ptr(dskip), K.ptr(dz), self.code, self.stream)
+        return dz
+
+    def backward(self, ctx, P, G, g_heads):
+        """g_heads: list of fp32 [N,H,W] grads of (out[, select, aux]) (None -> zeros).
+        Writes every parameter gradient into the tensors of dict G (fp32, reference layouts)."""
+        ctx.params = P
+        n, cin, H, W = ctx.shape
+        M = n * H * W
+        dev = ctx.x.device
+        bn = ctx.bn
+        heads = LY.HEADS if ctx.selective else LY.HEADS[:1]
+        gs = [g if g is not None else torch.zeros(n, H, W, dtype=torch.float32, device=dev) for g in g_heads]
+        gs = [g.contiguous() for g in gs] + [None] * (3 - len(gs))
+        d11 = bn["decoder_layer_1_1"]
+        dz = torch.empty(M, 64, dtype=self.dt, device=dev)
+        rows = K.query("selunet_channel_slab_rows", M)
+        nh = len(heads)
+        slab = torch.empty(rows, nh * 65, dtype=torch.float32, device=dev)
+        K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
+               K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), self.code, self.stream)
+        hsum = torch.empty(nh, 65, dtype=torch.float32, device=dev)
+        self._reduce(slab, rows, nh * 65, out32=hsum)
+        for i, h in enumerate(heads):
+            G[f"{h}.weight"].view(64).copy_(hsum[i, :64])
+            G[f"{h}.bias"].view(1).copy_(hsum[i, 64:])
+
+        e12, e22, e32 = bn["encoder_layer_1_2"], bn["encoder_layer_2_2"], bn["encoder_layer_3_2"]
+        u1, u2, u3 = ctx.ups["unpool1"], ctx.ups["unpool2"], ctx.ups["unpool3"]
+        p1, p2, p3 = ctx.pools["pool1"], ctx.pools["pool2"], ctx.pools["pool3"]
+        cb = lambda name, d, srcs, **kw: self._cbr_bwd(ctx, name, d, G, srcs, **kw)  # noqa: E731
+
+        dz = cb("decoder_layer_1_1", dz, [bn["decoder_layer_1_2"].src()])
+        du1, dskip1 = cb("decoder_layer_1_2", dz, [K.source(u1, 64), e12.src()], dgrad_split=64)
+        dz = self._up_bwd(ctx, "unpool1", du1, G, bn["decoder_layer_2_1"])
+        dz = cb("decoder_layer_2_1", dz, [bn["decoder_layer_2_2"].src()])
+        du2, dskip2 = cb("decoder_layer_2_2", dz, [K.source(u2, 128), e22.src()], dgrad_split=128)
+        dz = self._up_bwd(ctx, "unpool2", du2, G, bn["decoder_layer_3_1"])
+        dz = cb("decoder_layer_3_1", dz, [bn["decoder_layer_3_2"].src()])
+        du3, dskip3 = cb("decoder_layer_3_2", dz, [K.source(u3, 256), e32.src()], dgrad_split=256)
+        dz = self._up_bwd(ctx, "unpool3", du3, G, bn["decoder_layer_4_1"])
+        dz = cb("decoder_layer_4_1", dz, [bn["decoder_layer_4_2"].src()])
+        dp3 = cb("decoder_layer_4_2", dz, [K.source(p3, 256)])
+        dz = self._pool_bwd(e32, dp3, dskip3)
+        dz = cb("encoder_layer_3_2", dz, [bn["encoder_layer_3_1"].src()])
+        dp2 = cb("encoder_layer_3_1", dz, [K.source(p2, 128)])
+        dz = self._pool_bwd(e22, dp2, dskip2)
+        dz = cb("encoder_layer_2_2", dz, [bn["encoder_layer_2_1"].src()])
+        dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64)])
+        dz = self._pool_bwd(e12, dp1, dskip1)
+        dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()])
+        cb("encoder_layer_1_1", dz, [K.source(ctx.x, cin, layout=1)], need_dgrad=False)

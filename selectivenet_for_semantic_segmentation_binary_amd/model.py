@@ -1,0 +1,178 @@
+"""Drop-in `UNet_B` / `CBR_2D` (reference: model.py:9-103) backed by the MI355X kernels.
+
+Same constructor signature (`UNet_B(input_type='RGB', selective=False)`), same submodule
+names, parameter shapes and registration order (so `state_dict()` keys, checkpoints and Adam
+state indices are interchangeable with the reference), same forward contract: `[N,C,H,W]`
+fp32 in, `(N,H,W)` logits out, or the `(out, select, aux)` triple when selective
+(model.py:98-103). The modules inside `CBR_2D` are parameter containers only; the forward
+runs entirely in libselunet.so through one autograd.Function (`_UNetBFunction`).
+
+Extra keyword (not in the reference): `compute_dtype` — torch.float32 (default; exact fp32
+MFMA, the parity configuration) or torch.bfloat16 (bf16 operands, fp32 accumulation,
+statistics, losses and master weights).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib as K
+from . import layout as LY
+from . import parallel
+from .engine import Engine
+
+
+class _Conv2dParams(nn.Module):
+    """Holds Conv2d(in, out, k) parameters exactly as nn.Conv2d registers them."""
+
+    def __init__(self, in_ch, out_ch, k):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = in_ch, out_ch, (k, k)
+        self.weight = nn.Parameter(torch.empty(out_ch, in_ch, k, k))
+        self.bias = nn.Parameter(torch.empty(out_ch))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # torch.nn.Conv2d default init (kaiming_uniform_(a=sqrt(5)) and fan_in-bounded bias)
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(self.weight[0].numel())
+        nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):  # pragma: no cover - the whole network runs as one fused Function
+        raise RuntimeError("submodules of the MI355X UNet_B are parameter containers; call the UNet_B module")
+
+
+class _ConvTranspose2dParams(_Conv2dParams):
+    def __init__(self, in_ch, out_ch, k):
+        nn.Module.__init__(self)
+        self.in_channels, self.out_channels, self.kernel_size = in_ch, out_ch, (k, k)
+        self.weight = nn.Parameter(torch.empty(in_ch, out_ch, k, k))
+        self.bias = nn.Parameter(torch.empty(out_ch))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(out_ch * k * k)
+        nn.init.uniform_(self.bias, -bound, bound)
+
+
+class _BatchNorm2dParams(nn.Module):
+    """BatchNorm2d(num_features) parameters and buffers (eps 1e-5, momentum 0.1)."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = c, 1e-5, 0.1
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def forward(self, x):  # pragma: no cover
+        raise RuntimeError("parameter container")
+
+
+class _ReLU(nn.Module):
+    def forward(self, x):  # pragma: no cover
+        raise RuntimeError("parameter container")
+
+
+def CBR_2D(in_ch, out_ch, k_size=3, stride=1, padding=1, bias=True):
+    """model.py:9-15: Sequential(Conv2d, BatchNorm2d, ReLU) — here as parameter containers
+    (only the reference's arguments k_size=3, stride=1, padding=1, bias=True are supported)."""
+    if (k_size, stride, padding, bias) != (3, 1, 1, True):
+        raise NotImplementedError("the MI355X CBR_2D implements conv3x3 / stride 1 / pad 1 / bias (model.py:9)")
+    return nn.Sequential(_Conv2dParams(in_ch, out_ch, 3), _BatchNorm2dParams(out_ch), _ReLU())
+
+
+class _UNetBFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        names = module._param_names
+        P = dict(zip(names, params))
+        B = dict(module.named_buffers())
+        training = module.training
+        if not training and parallel.is_initialized():
+            parallel.broadcast_buffers(module)  # DataParallel replicas read device 0's buffers
+        eng = module._engine()
+        need_bwd = training and any(ctx.needs_input_grad[2:])
+        outs, ectx = eng.forward(x.contiguous(), P, B, module.selective, training, need_backward=need_bwd)
+        if need_bwd:
+            ctx.ectx = ectx
+            ctx.eng = eng
+            ctx.names = names
+            ctx.P = P
+        else:
+            ctx.ectx = None
+        return outs if len(outs) > 1 else outs[0]
+
+    @staticmethod
+    def backward(ctx, *g_heads):
+        if ctx.ectx is None:
+            raise RuntimeError("UNet_B backward needs a training-mode forward with grad enabled")
+        names, P = ctx.names, ctx.P
+        dev = g_heads[0].device if g_heads[0] is not None else next(iter(P.values())).device
+        total = sum(P[n].numel() for n in names)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        G, off = {}, 0
+        for n in names:
+            k = P[n].numel()
+            G[n] = flat[off:off + k].view(P[n].shape)
+            off += k
+        ctx.eng.backward(ctx.ectx, P, G, list(g_heads))
+        ctx.ectx = None
+        if parallel.is_initialized():
+            parallel.allreduce_grads(flat)  # DataParallel reduce-add of replica gradients
+        return (None, None, *[G[n] for n in names])
+
+
+class UNet_B(nn.Module):
+    """model.py:18-103 UNet for BCE loss, optionally SelectiveNet (selection + aux heads)."""
+
+    def __init__(self, input_type="RGB", selective=False, compute_dtype=torch.float32):
+        super().__init__()
+        self.selective = selective
+        input_ch = LY.input_channels(input_type)
+        self.compute_dtype = compute_dtype
+
+        self.encoder_layer_1_1 = CBR_2D(in_ch=input_ch, out_ch=64)
+        self.encoder_layer_1_2 = CBR_2D(in_ch=64, out_ch=64)
+        self.pool1 = nn.Identity()
+        self.encoder_layer_2_1 = CBR_2D(in_ch=64, out_ch=128)
+        self.encoder_layer_2_2 = CBR_2D(in_ch=128, out_ch=128)
+        self.pool2 = nn.Identity()
+        self.encoder_layer_3_1 = CBR_2D(in_ch=128, out_ch=256)
+        self.encoder_layer_3_2 = CBR_2D(in_ch=256, out_ch=256)
+        self.pool3 = nn.Identity()
+        self.decoder_layer_4_2 = CBR_2D(in_ch=256, out_ch=512)
+        self.decoder_layer_4_1 = CBR_2D(in_ch=512, out_ch=512)
+        self.unpool3 = _ConvTranspose2dParams(512, 256, 2)
+        self.decoder_layer_3_2 = CBR_2D(in_ch=512, out_ch=256)
+        self.decoder_layer_3_1 = CBR_2D(in_ch=256, out_ch=256)
+        self.unpool2 = _ConvTranspose2dParams(256, 128, 2)
+        self.decoder_layer_2_2 = CBR_2D(in_ch=256, out_ch=128)
+        self.decoder_layer_2_1 = CBR_2D(in_ch=128, out_ch=128)
+        self.unpool1 = _ConvTranspose2dParams(128, 64, 2)
+        self.decoder_layer_1_2 = CBR_2D(in_ch=128, out_ch=64)
+        self.decoder_layer_1_1 = CBR_2D(in_ch=64, out_ch=64)
+        self.conv1x1 = _Conv2dParams(64, 1, 1)
+        if self.selective:
+            self.conv_select = _Conv2dParams(64, 1, 1)
+            self.conv_aux = _Conv2dParams(64, 1, 1)
+        self._param_names = [n for n, _ in self.named_parameters()]
+        self._engines = {}
+
+    def _engine(self):
+        e = self._engines.get(self.compute_dtype)
+        if e is None:
+            e = self._engines[self.compute_dtype] = Engine(self.compute_dtype)
+        return e
+
+    def forward(self, x):
+        if x.device.type != "cuda":
+            raise RuntimeError("the MI355X UNet_B runs on the GPU only (no CPU fallback); move the model and "
+                               "input to a cuda device")
+        K.load()
+        params = [p for _, p in self.named_parameters()]
+        if x.dtype != torch.float32:
+            x = x.float()
+        return _UNetBFunction.apply(x, self, *params)

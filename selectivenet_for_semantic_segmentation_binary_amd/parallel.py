@@ -1,0 +1,110 @@
+"""Data parallelism: one process per GPU replacing `torch.nn.DataParallel` (train.py:131-134).
+
+The reference runs single-process DataParallel: the global batch is scattered in contiguous
+chunks (torch.chunk semantics), each replica runs BatchNorm on its own chunk, the three head
+outputs are gathered to cuda:0 where the selective loss is evaluated on the *global* batch,
+gradients are reduce-added to cuda:0, and only replica 0's BN running statistics persist.
+
+Here each rank owns one GPU and one chunk. The exchange steps are exactly the ones the
+math needs:
+  * forward: all-reduce (sum) of the loss partial sums — 2 doubles for the selective risk
+    (sum sigmoid(g), sum ell*sigmoid(g)) + the pixel count, 1 for the aux BCE — so every rank
+    sees the global-batch loss and computes its local per-pixel gradients with the global
+    normalisers;
+  * backward: all-reduce (sum, not mean) of the flat fp32 gradient buffer (30.8 MB);
+  * eval: rank 0's BN buffers broadcast before an eval-mode forward (DataParallel re-broadcasts
+    device-0 buffers every forward).
+Backend "nccl" is RCCL on ROCm (xGMI within a node); "gloo" is used by the CPU tests.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+_STATE = {"enabled": False, "group": None}
+
+
+def init_data_parallel(backend: str | None = None, group=None) -> tuple[int, int]:
+    """Initialise (if needed) the default process group from RANK/WORLD_SIZE/MASTER_* env vars
+    and enable the data-parallel exchanges. Returns (rank, world_size)."""
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+    _STATE["enabled"] = dist.get_world_size(group) > 1
+    _STATE["group"] = group
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def disable():
+    _STATE["enabled"] = False
+    _STATE["group"] = None
+
+
+def is_initialized() -> bool:
+    return _STATE["enabled"] and dist.is_initialized()
+
+
+def world_size() -> int:
+    return dist.get_world_size(_STATE["group"]) if is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank(_STATE["group"]) if is_initialized() else 0
+
+
+def allreduce_sums(t: torch.Tensor) -> torch.Tensor:
+    """In-place global sum of a small partial-sum vector (loss forward exchange)."""
+    if is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_STATE["group"])
+    return t
+
+
+def allreduce_grads(flat: torch.Tensor, bucket_elems: int = 1 << 22) -> torch.Tensor:
+    """Sum replica gradients (DataParallel reduce_add semantics), in buckets."""
+    if not is_initialized():
+        return flat
+    n = flat.numel()
+    works = []
+    for off in range(0, n, bucket_elems):
+        works.append(dist.all_reduce(flat[off:off + bucket_elems], op=dist.ReduceOp.SUM, group=_STATE["group"],
+                                     async_op=True))
+    for w in works:
+        w.wait()
+    return flat
+
+
+def broadcast_buffers(module: torch.nn.Module):
+    if not is_initialized():
+        return
+    for b in module.buffers():
+        dist.broadcast(b, src=0, group=_STATE["group"])
+
+
+def broadcast_params(module: torch.nn.Module):
+    """Make every rank start from rank 0's parameters and buffers."""
+    if not dist.is_initialized():
+        return
+    with torch.no_grad():
+        for p in module.parameters():
+            dist.broadcast(p.data, src=0, group=_STATE["group"])
+        for b in module.buffers():
+            dist.broadcast(b, src=0, group=_STATE["group"])
+
+
+def chunk_bounds(batch: int, rank_: int, world: int) -> tuple[int, int]:
+    """Rows [lo, hi) of replica `rank_` under DataParallel's scatter (torch.chunk on dim 0:
+    chunks of ceil(batch / world), the last ones possibly shorter or empty)."""
+    size = -(-batch // world)
+    lo = min(batch, rank_ * size)
+    hi = min(batch, lo + size)
+    return lo, hi
+
+
+def local_batch(x: torch.Tensor, rank_: int | None = None, world: int | None = None) -> torch.Tensor:
+    r = rank() if rank_ is None else rank_
+    w = world_size() if world is None else world
+    lo, hi = chunk_bounds(x.shape[0], r, w)
+    return x[lo:hi]

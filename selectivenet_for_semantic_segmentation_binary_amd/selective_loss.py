@@ -1,0 +1,148 @@
+"""Selective risk and aux BCE on the MI355X (reference: selective_loss.py:58-85, train.py:78,195).
+
+`calc_selective_risk_image_b(output, selection, target, target_coverage=0.8, lamb=8,
+hard_selection=False) -> (loss, coverage)` keeps the reference signature and return values:
+
+    s = sigmoid(selection); coverage = mean(s)
+    risk = -mean((t*log(sigmoid(x)) + (1-t)*log(1-sigmoid(x))) * s) / coverage
+    loss = risk + lamb * max(target_coverage - coverage, 0)^2
+
+computed by wavefront-reduced HIP kernels (partials -> deterministic fp64 reduce -> scalar
+finalize) with log(sigmoid(x)) = -softplus(-x) and log(1-sigmoid(x)) = -softplus(x). This equals
+the reference wherever the reference is finite; the reference's literal fp32 form returns NaN as
+soon as a logit saturates (|x| > ~16.6) and loses digits from |x| ~ 9 on.
+
+Under data parallelism (parallel.init_data_parallel) the partial sums are all-reduced, so loss
+and coverage are those of the global batch — what DataParallel computes after gathering the
+outputs to cuda:0 — and each rank back-propagates its own pixels with the global normalisers.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib as K
+from . import parallel
+
+
+def _check(t, name):
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be a cuda tensor (the MI355X losses have no CPU fallback)")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _reduced_sums(slab, rows, cols):
+    """fp64 column sums of a partial slab, all-reduced across data-parallel ranks."""
+    sums = torch.empty(cols, dtype=torch.float64, device=slab.device)
+    ws = torch.empty(K.query("selunet_reduce_ws_bytes", cols) // 8, dtype=torch.float64, device=slab.device)
+    K.call("selunet_reduce_rows", K.ptr(slab), rows, cols, K.ptr(ws), K.ptr(sums), None, K.stream_ptr())
+    parallel.allreduce_sums(sums)
+    return sums
+
+
+def _global_count(p_local: int) -> float:
+    if not parallel.is_initialized():
+        return float(p_local)
+    t = torch.tensor([float(p_local)], dtype=torch.float64,
+                     device="cuda" if torch.cuda.is_available() else "cpu")
+    parallel.allreduce_sums(t)
+    return float(t.item())
+
+
+_COUNT_CACHE = {}
+
+
+def global_count(p_local: int) -> float:
+    """Global pixel count of the data-parallel batch (cached per local size and world)."""
+    key = (p_local, parallel.world_size())
+    if key not in _COUNT_CACHE:
+        _COUNT_CACHE[key] = _global_count(p_local)
+    return _COUNT_CACHE[key]
+
+
+class _SelectiveRiskB(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, output, selection, target, target_coverage, lamb):
+        p = output.numel()
+        dev = output.device
+        rows = K.query("selunet_loss_slab_rows", p)
+        slab = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        K.call("selunet_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), p, K.ptr(slab),
+               K.stream_ptr())
+        sums = _reduced_sums(slab, rows, 2)
+        p_global = global_count(p)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        coverage = torch.empty((), dtype=torch.float32, device=dev)
+        state = torch.empty(4, dtype=torch.float32, device=dev)
+        K.call("selunet_selective_finalize", K.ptr(sums), p_global, float(lamb), float(target_coverage), K.ptr(loss),
+               K.ptr(coverage), K.ptr(state), K.stream_ptr())
+        ctx.save_for_backward(output, selection, target, state)
+        ctx.lamb = float(lamb)
+        return loss, coverage
+
+    @staticmethod
+    def backward(ctx, g_loss, g_cov):
+        output, selection, target, state = ctx.saved_tensors
+        d_out = torch.empty_like(output)
+        d_sel = torch.empty_like(selection)
+        gl = g_loss.contiguous().float() if g_loss is not None else None
+        gc = g_cov.contiguous().float() if g_cov is not None else None
+        K.call("selunet_selective_bwd", K.ptr(output), K.ptr(selection), K.ptr(target), output.numel(), K.ptr(state),
+               ctx.lamb, K.ptr(gl), K.ptr(gc), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
+        return d_out, d_sel, None, None, None
+
+
+def calc_selective_risk_image_b(output, selection, target, target_coverage=0.8, lamb=8, hard_selection=False):
+    """selective_loss.py:58-85 (BCE-with-logits selective risk). output/selection/target: (N, H, W)."""
+    if hard_selection:
+        raise NotImplementedError("hard_selection=True (selective_loss.py:74-77) is not on the training path "
+                                  "(train.py:196 never sets it) and is not implemented on the MI355X path")
+    if output.shape != selection.shape or output.shape != target.shape:
+        raise ValueError(f"shape mismatch: output {tuple(output.shape)}, selection {tuple(selection.shape)}, "
+                         f"target {tuple(target.shape)}")
+    o, s, t = _check(output, "output"), _check(selection, "selection"), _check(target, "target")
+    return _SelectiveRiskB.apply(o, s, t, target_coverage, lamb)
+
+
+class _BCEWithLogitsMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logit, target):
+        p = logit.numel()
+        dev = logit.device
+        rows = K.query("selunet_loss_slab_rows", p)
+        slab = torch.empty(rows, 1, dtype=torch.float32, device=dev)
+        K.call("selunet_bce_partials", K.ptr(logit), K.ptr(target), p, K.ptr(slab), K.stream_ptr())
+        sums = _reduced_sums(slab, rows, 1)
+        p_global = global_count(p)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        K.call("selunet_bce_finalize", K.ptr(sums), p_global, K.ptr(loss), K.stream_ptr())
+        ctx.save_for_backward(logit, target)
+        ctx.p_global = p_global
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logit, target = ctx.saved_tensors
+        d = torch.empty_like(logit)
+        g = g.contiguous().float()  # keep alive until the launch is enqueued
+        K.call("selunet_bce_bwd", K.ptr(logit), K.ptr(target), logit.numel(), ctx.p_global, K.ptr(g), K.ptr(d),
+               K.stream_ptr())
+        return d, None
+
+
+class BCEWithLogitsLoss(nn.Module):
+    """torch.nn.BCEWithLogitsLoss() with the default reduction='mean' (train.py:78)."""
+
+    def __init__(self, weight=None, size_average=None, reduce=None, reduction="mean", pos_weight=None):
+        super().__init__()
+        if weight is not None or pos_weight is not None or reduction != "mean" or size_average is not None \
+                or reduce is not None:
+            raise NotImplementedError("only the reference's BCEWithLogitsLoss() (mean, unweighted) is implemented")
+
+    def forward(self, input, target):
+        if input.shape != target.shape:
+            raise ValueError(f"Target size ({tuple(target.shape)}) must be the same as input size "
+                             f"({tuple(input.shape)})")
+        return _BCEWithLogitsMean.apply(_check(input, "input"), _check(target, "target"))

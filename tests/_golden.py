@@ -55,3 +55,40 @@ def max_rel(got, ref):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def check_grads_vs_truth(d, grads, floor=1e-4, factor=3.0, skip=()):
+    """Gradient parity measured against the reference's own fp64 run (`s0/grad64*`).
+
+    For each tensor: e_ref = max|g_ref32 - g64| / max|g64| over the fixture's samples (the
+    reference's own fp32 error), e_ours likewise; pass when e_ours <= max(floor, factor*e_ref).
+    The same for the tensor norms. Returns (failures, report) where report lists
+    (name, e_ours, e_ref) sorted by e_ours."""
+    fails, report = [], []
+    for name in tensor_keys(d, "s0/grad"):
+        if name in skip:
+            continue
+        a = np.asarray(grads[name], np.float64).ravel()
+        if "s0/gradfull/" + name in d.files:
+            ref32 = d["s0/gradfull/" + name].astype(np.float64)
+            g64 = d["s0/grad64full/" + name]
+            got = a
+        else:
+            idx = d["s0/gradidx/" + name]
+            ref32 = d["s0/gradval/" + name].astype(np.float64)
+            g64 = d["s0/grad64val/" + name]
+            got = a[idx]
+        scale = max(np.abs(g64).max(), 1e-30)
+        e_ref = float(np.abs(ref32 - g64).max() / scale)
+        e_ours = float(np.abs(got - g64).max() / scale)
+        n64 = float(d["s0/grad64norm/" + name])
+        n_ref = float(d["s0/gradnorm/" + name])
+        en_ref = abs(n_ref - n64) / max(n64, 1e-30)
+        en_ours = abs(float(np.linalg.norm(a)) - n64) / max(n64, 1e-30)
+        report.append((name, e_ours, e_ref))
+        if e_ours > max(floor, factor * e_ref):
+            fails.append(f"{name}: sample err vs fp64 {e_ours:.2e} > max({floor:g}, {factor:g} x ref {e_ref:.2e})")
+        if en_ours > max(floor, factor * en_ref):
+            fails.append(f"{name}: norm err vs fp64 {en_ours:.2e} > max({floor:g}, {factor:g} x ref {en_ref:.2e})")
+    report.sort(key=lambda r: -r[1])
+    return fails, report

@@ -41,7 +41,7 @@ import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E4
 from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch  # noqa: E402
 
 torch.set_num_threads(8)
-N_SAMPLES = 64
+N_SAMPLES = 128
 
 
 def build_ref(seed, selective, input_type="RGB"):
@@ -109,6 +109,26 @@ def ref_step(net, optim, x, lab, selective, lamb, chunks=1):
     return res
 
 
+def fp64_truth(out, n, size, selective, lamb, chunks, seed, data_seed):
+    """Step 0 of the same reference iteration in float64 (net.double()): the 'truth' that
+    both fp32 implementations are measured against (ReLU-mask / max-pool-argmax near-ties make
+    fp32 gradients differ from it by up to a few % of a tensor's max, reference included)."""
+    x, lab = make_batch(n, size, seed=data_seed)
+    net = build_ref(seed, selective).double()
+    net.train()
+    optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+    r = ref_step(net, optim, torch.tensor(x, dtype=torch.float64), torch.tensor(lab, dtype=torch.float64),
+                 selective, lamb, chunks)
+    out["s0/loss64"] = np.float64(r["loss"].item())
+    for k, t in r["grads"].items():
+        a = t.numpy().astype(np.float64).ravel()
+        out[f"s0/grad64norm/{k}"] = np.float64(np.linalg.norm(a))
+        if f"s0/gradfull/{k}" in out:
+            out[f"s0/grad64full/{k}"] = a
+        else:
+            out[f"s0/grad64val/{k}"] = a[out[f"s0/gradidx/{k}"]]
+
+
 def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outputs=True, seed=0, data_seed=1):
     x, lab = make_batch(n, size, seed=data_seed)
     xt, lt = torch.tensor(x), torch.tensor(lab)
@@ -150,6 +170,7 @@ def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outp
         for k, v in bufs.items():
             out[pre + "buf/" + k] = v.numpy().astype(np.float32)
         out[pre + "num_batches_tracked"] = np.int64(net.state_dict()["encoder_layer_1_1.1.num_batches_tracked"].item())
+    fp64_truth(out, n, size, selective, lamb, chunks, seed, data_seed)
     path = os.path.join(HERE, fname)
     np.savez_compressed(path, **out)
     print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB)")

@@ -1,0 +1,362 @@
+"""Per-kernel parity of libselunet.so against plain PyTorch fp32 on the CPU (the oracle's ops).
+
+Called through the C-ABI (ctypes) exactly as the product path calls it. fp32 tolerance:
+1e-4 relative to the tensor's max magnitude; exact fp32 MFMA accumulation differs from
+oneDNN's summation order only in rounding.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from selectivenet_for_semantic_segmentation_binary_amd import _lib as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-4
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max(), 1e-30))
+
+
+def nhwc(t):  # [N,C,H,W] -> [N*H*W, C]
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).contiguous()
+
+
+def nchw(t, n, h, w):
+    return t.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def gen(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def bn_fold(c, seed):
+    scale = gen(c, seed=seed).abs() + 0.5
+    shift = gen(c, seed=seed + 1) * 0.3
+    return scale, shift
+
+
+def pack(w, dt=torch.float32):
+    co, ci = w.shape[:2]
+    bke = 128 // torch.empty((), dtype=dt).element_size()
+    kpad = (9 * ci + bke - 1) // bke * bke
+    fwd = torch.empty(co, kpad, dtype=dt, device=DEV)
+    dg = torch.empty(ci, 9 * co, dtype=dt, device=DEV)
+    wd = w.to(DEV).contiguous()
+    K.call("selunet_pack_conv3x3", K.ptr(wd), co, ci, kpad, K.ptr(fwd), K.ptr(dg), K.dtype_code(dt), K.stream_ptr())
+    return fwd, dg, kpad
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,n,h,w,xform", [
+    (64, 0, 64, 2, 16, 16, True),
+    (128, 0, 256, 1, 8, 12, False),
+    (64, 64, 128, 2, 8, 8, True),      # two-source (torch.cat) gather
+    (256, 256, 256, 1, 4, 4, True),
+    (64, 0, 128, 3, 5, 7, True),       # M not a multiple of the 128-row tile
+])
+def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform):
+    x0 = gen(n, cin0, h, w, seed=1)
+    x1 = gen(n, cin1, h, w, seed=2) if cin1 else None
+    wt = gen(cout, cin0 + cin1, 3, 3, seed=3, scale=0.05)
+    s0, t0 = bn_fold(cin0, 10)
+    s1, t1 = bn_fold(cin1, 12) if cin1 else (None, None)
+    # reference: transform (BN fold + relu) applied to source 1 only when it is a "skip" source
+    a0 = torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)) if xform else x0
+    a = a0
+    if cin1:
+        a1 = torch.relu(x1 * s1.view(1, -1, 1, 1) + t1.view(1, -1, 1, 1))
+        a = torch.cat((a0, a1), 1)
+    ref = F.conv2d(a, wt, padding=1)
+    fwd, _, kpad = pack(wt)
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    x0d, s0d, t0d = d(nhwc(x0)), d(s0), d(t0)
+    srcs = [K.source(x0d, cin0, s0d if xform else None, t0d if xform else None)]
+    if cin1:
+        x1d, s1d, t1d = d(nhwc(x1)), d(s1), d(t1)
+        srcs.append(K.source(x1d, cin1, s1d, t1d))
+    M = n * h * w
+    y = torch.empty(M, cout, device=DEV)
+    rows = (M + 127) // 128
+    stats = torch.empty(rows, 2, cout, device=DEV)
+    ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 9, *srcs), K.ptr(fwd), cout, kpad, ep, K.F32, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel(nchw(y.cpu(), n, h, w), ref) < TOL
+    st = stats.cpu().double().sum(0)
+    r = ref.double().permute(1, 0, 2, 3).reshape(cout, -1)
+    assert rel(st[0], r.sum(1)) < TOL and rel(st[1], (r * r).sum(1)) < TOL
+
+
+def test_conv3x3_fwd_small_c_nchw():
+    n, h, w = 2, 16, 16
+    x = gen(n, 3, h, w, seed=4)
+    wt = gen(64, 3, 3, 3, seed=5, scale=0.2)
+    ref = F.conv2d(x, wt, padding=1)
+    fwd, _, kpad = pack(wt)
+    xd = x.to(DEV).contiguous()
+    y = torch.empty(n * h * w, 64, device=DEV)
+    ep = K.Epilogue(K.ptr(y), None, None, None, K.EP_PLAIN, 0)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 9, K.source(xd, 3, layout=1)), K.ptr(fwd), 64, kpad, ep, K.F32,
+           K.stream_ptr())
+    assert rel(nchw(y.cpu(), n, h, w), ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,split", [(64, 64, 0), (128, 64, 64), (512, 256, 256), (64, 128, 0)])
+def test_conv3x3_dgrad(cin, cout, split):
+    n, h, w = 2, 8, 8
+    wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
+    dy = gen(n, cout, h, w, seed=7)
+    x = gen(n, cin, h, w, seed=8).requires_grad_()
+    y = F.conv2d(x, wt, padding=1)
+    (ref,) = torch.autograd.grad(y, x, dy)
+    _, dg, _ = pack(wt)
+    dyd = nhwc(dy).to(DEV)
+    M = n * h * w
+    g = K.gather(n, h, w, 9, K.source(dyd, cout))
+    if split:
+        d0 = torch.empty(M, split, device=DEV)
+        d1 = torch.empty(M, cin - split, device=DEV)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split)
+        K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.F32, K.stream_ptr())
+        got = torch.cat((nchw(d0.cpu(), n, h, w), nchw(d1.cpu(), n, h, w)), 1)
+    else:
+        dx = torch.empty(M, cin, device=DEV)
+        ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+        K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.F32, K.stream_ptr())
+        got = nchw(dx.cpu(), n, h, w)
+    assert rel(got, ref) < TOL
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,xform,small", [(64, 0, 64, True, False), (64, 64, 128, True, False),
+                                                        (128, 0, 256, False, False), (3, 0, 64, False, True)])
+def test_conv3x3_wgrad(cin0, cin1, cout, xform, small):
+    n, h, w = 2, 16, 16
+    x0 = gen(n, cin0, h, w, seed=9)
+    x1 = gen(n, cin1, h, w, seed=10) if cin1 else None
+    s0, t0 = bn_fold(cin0, 20)
+    s1, t1 = bn_fold(cin1, 22) if cin1 else (None, None)
+    a = torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)) if xform else x0
+    if cin1:
+        a = torch.cat((a, torch.relu(x1 * s1.view(1, -1, 1, 1) + t1.view(1, -1, 1, 1))), 1)
+    cin = cin0 + cin1
+    wt = gen(cout, cin, 3, 3, seed=11, scale=0.05).requires_grad_()
+    dy = gen(n, cout, h, w, seed=12)
+    y = F.conv2d(a, wt, padding=1)
+    (ref,) = torch.autograd.grad(y, wt, dy)
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    if small:
+        srcs = [K.source(d(x0), cin0, layout=1)]
+        keep = [d(x0)]
+        srcs = [K.source(keep[0], cin0, layout=1)]
+    else:
+        keep = [d(nhwc(x0)), d(s0), d(t0)]
+        srcs = [K.source(keep[0], cin0, keep[1] if xform else None, keep[2] if xform else None)]
+        if cin1:
+            keep += [d(nhwc(x1)), d(s1), d(t1)]
+            srcs.append(K.source(keep[3], cin1, keep[4], keep[5]))
+    dyd = d(nhwc(dy))
+    ld = K.query("selunet_wgrad_ld", 9 * cin)
+    packed = torch.zeros(cout, ld, device=DEV)
+    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs),
+           K.ptr(packed), K.F32, K.stream_ptr())
+    out = torch.empty(cout, cin, 3, 3, device=DEV)
+    K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cout, cin, ld, K.ptr(out), K.stream_ptr())
+    assert rel(out.cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64)])
+def test_convT_fwd_bwd(cin, cout):
+    n, h, w = 2, 4, 6
+    x = gen(n, cin, h, w, seed=13)
+    s, t = bn_fold(cin, 30)
+    a = torch.relu(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1)).requires_grad_()
+    wt = gen(cin, cout, 2, 2, seed=14, scale=0.05).requires_grad_()
+    b = gen(cout, seed=15).requires_grad_()
+    y = F.conv_transpose2d(a, wt, b, stride=2)
+    dy = gen(*y.shape, seed=16)
+    ga, gw, gb = torch.autograd.grad(y, (a, wt, b), dy)
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    xd, sd, td, wd, bd = d(nhwc(x)), d(s), d(t), d(wt.detach()), d(b.detach())
+    fwd = torch.empty(4 * cout, cin, device=DEV)
+    dg = torch.empty(cin, 4 * cout, device=DEV)
+    K.call("selunet_pack_convT", K.ptr(wd), cin, cout, K.ptr(fwd), K.ptr(dg), K.F32, K.stream_ptr())
+    up = torch.empty(n * 2 * h * 2 * w, cout, device=DEV)
+    ep = K.Epilogue(K.ptr(up), None, K.ptr(bd), None, K.EP_SCATTER2X, 0)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 1, K.source(xd, cin, sd, td)), K.ptr(fwd), 4 * cout, cin, ep,
+           K.F32, K.stream_ptr())
+    assert rel(nchw(up.cpu(), n, 2 * h, 2 * w), y) < TOL
+    # backward
+    dud = d(nhwc(dy))
+    da = torch.empty(n * h * w, cin, device=DEV)
+    ep = K.Epilogue(K.ptr(da), None, None, None, K.EP_PLAIN, 0)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 4, K.source(dud, cout)), K.ptr(dg), cin, 4 * cout, ep, K.F32,
+           K.stream_ptr())
+    assert rel(nchw(da.cpu(), n, h, w), ga) < TOL
+    ld = K.query("selunet_wgrad_ld", 4 * cout)
+    packed = torch.zeros(cin, ld, device=DEV)
+    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(xd, cin, sd, td)),
+           K.gather(n, h, w, 4, K.source(dud, cout)), K.ptr(packed), K.F32, K.stream_ptr())
+    gwd = torch.empty(cin, cout, 2, 2, device=DEV)
+    K.call("selunet_unpack_convT_grad", K.ptr(packed), cin, cout, K.ptr(gwd), K.stream_ptr())
+    assert rel(gwd.cpu(), gw) < TOL
+    Mu = n * 4 * h * w
+    rows = K.query("selunet_channel_slab_rows", Mu)
+    slab = torch.empty(rows, cout, device=DEV)
+    K.call("selunet_channel_sum", K.ptr(dud), Mu, cout, K.ptr(slab), K.F32, K.stream_ptr())
+    assert rel(slab.sum(0).cpu(), gb) < TOL
+
+
+def test_maxpool_ties_and_backward():
+    """Windows with exact ties (post-ReLU zeros, duplicated maxima): gradient goes to the first
+    maximum in row-major window order, as ATen's max_pool2d_with_indices."""
+    n, c, h, w = 2, 64, 8, 8
+    y = gen(n, c, h, w, seed=17)
+    y[:, :, ::2, 1::2] = y[:, :, ::2, ::2]          # tie between (0,0) and (0,1)
+    y[:, :8] = -1.0                                  # all-zero windows after ReLU
+    s = torch.ones(c)
+    t = torch.zeros(c)
+    z = torch.relu(y).requires_grad_()
+    p = F.max_pool2d(z, 2)
+    dp = gen(*p.shape, seed=18)
+    dskip = gen(*z.shape, seed=19)
+    (gz,) = torch.autograd.grad(p, z, dp)
+    gz = gz + dskip
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    yd, sd, td = d(nhwc(y)), d(s), d(t)
+    out = torch.empty(n * h * w // 4, c, device=DEV)
+    K.call("selunet_maxpool2_fwd", K.ptr(yd), n, h, w, c, K.ptr(sd), K.ptr(td), K.ptr(out), K.F32, K.stream_ptr())
+    assert torch.equal(nchw(out.cpu(), n, h // 2, w // 2), p.detach())
+    dpd, dsd = d(nhwc(dp)), d(nhwc(dskip))
+    dz = torch.empty_like(yd)
+    K.call("selunet_maxpool2_bwd", K.ptr(yd), n, h, w, c, K.ptr(sd), K.ptr(td), K.ptr(dpd), K.ptr(dsd), K.ptr(dz),
+           K.F32, K.stream_ptr())
+    assert torch.equal(nchw(dz.cpu(), n, h, w), gz)
+
+
+def test_bn_forward_backward_against_torch():
+    n, c, h, w = 4, 128, 8, 8
+    M = n * h * w
+    yr = gen(n, c, h, w, seed=20) * 2 + 0.5         # pre-BN conv output without bias
+    bias = gen(c, seed=21) * 0.1
+    gamma = gen(c, seed=22).abs() + 0.5
+    beta = gen(c, seed=23) * 0.2
+    rm0, rv0 = gen(c, seed=24) * 0.1, gen(c, seed=25).abs() + 0.5
+    yb = (yr + bias.view(1, -1, 1, 1)).requires_grad_()
+    gam = gamma.clone().requires_grad_()
+    bet = beta.clone().requires_grad_()
+    rm, rv = rm0.clone(), rv0.clone()
+    z = torch.relu(F.batch_norm(yb, rm, rv, gam, bet, training=True, momentum=0.1, eps=1e-5))
+    dz = gen(*z.shape, seed=26)
+    g_y, g_gam, g_bet = torch.autograd.grad(z, (yb, gam, bet), dz)
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    yd = d(nhwc(yr))
+    r = yr.double().permute(1, 0, 2, 3).reshape(c, -1)
+    sums = d(torch.cat([r.sum(1), (r * r).sum(1)]))
+    rmd, rvd = d(rm0), d(rv0)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    mean, invstd, scale, shift = (torch.empty(c, device=DEV) for _ in range(4))
+    biasd, gammad, betad = d(bias), d(gamma), d(beta)  # keep device tensors alive across the launch
+    K.call("selunet_bn_finalize", K.ptr(sums), M, c, K.ptr(biasd), K.ptr(gammad), K.ptr(betad), K.ptr(rmd),
+           K.ptr(rvd), K.ptr(nbt), 0.1, 1e-5, 1, K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift),
+           K.stream_ptr())
+    assert rel(rmd.cpu(), rm) < 1e-5 and rel(rvd.cpu(), rv) < 1e-5 and int(nbt) == 1
+    zz = torch.relu(yd * scale + shift)
+    assert rel(nchw(zz.cpu(), n, h, w), z) < TOL
+    dzd = d(nhwc(dz))
+    rows = K.query("selunet_channel_slab_rows", M)
+    slab = torch.empty(rows, 3, c, device=DEV)
+    K.call("selunet_bn_bwd_reduce", K.ptr(dzd), K.ptr(yd), M, c, K.ptr(scale), K.ptr(shift), K.ptr(mean),
+           K.ptr(invstd), K.ptr(slab), K.F32, K.stream_ptr())
+    s3 = slab.double().sum(0).reshape(-1).contiguous()
+    dgam, dbet, dbias = (torch.empty(c, device=DEV) for _ in range(3))
+    coef = torch.empty(3, c, device=DEV)
+    K.call("selunet_bn_bwd_finalize", K.ptr(s3), M, c, K.ptr(gammad), K.ptr(invstd), K.ptr(dgam), K.ptr(dbet),
+           K.ptr(dbias), K.ptr(coef), K.stream_ptr())
+    assert rel(dgam.cpu(), g_gam) < TOL and rel(dbet.cpu(), g_bet) < TOL
+    dy = torch.empty_like(yd)
+    K.call("selunet_bn_bwd_apply", K.ptr(dzd), K.ptr(yd), M, c, K.ptr(scale), K.ptr(shift), K.ptr(mean),
+           K.ptr(invstd), K.ptr(coef), K.ptr(dy), K.F32, K.stream_ptr())
+    assert rel(nchw(dy.cpu(), n, h, w), g_y) < TOL
+    assert float(dbias.abs().max()) < 1e-4 * float(g_y.abs().sum(dim=(0, 2, 3)).max() + 1)
+
+
+def test_reduce_rows_deterministic():
+    slab = gen(3001, 70, seed=27).to(DEV)
+    ws = torch.empty(K.query("selunet_reduce_ws_bytes", 70) // 8, dtype=torch.float64, device=DEV)
+    outs = []
+    for _ in range(2):
+        o = torch.empty(70, dtype=torch.float64, device=DEV)
+        K.call("selunet_reduce_rows", K.ptr(slab), 3001, 70, K.ptr(ws), K.ptr(o), None, K.stream_ptr())
+        outs.append(o.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert rel(outs[0], slab.double().sum(0).cpu()) < 1e-12
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,small", [(64, 0, 64, False), (64, 64, 128, False), (256, 0, 512, False),
+                                                  (3, 0, 64, True)])
+def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small):
+    """bf16 operands, fp32 accumulation: compared with fp32 torch on the same bf16-rounded data."""
+    n, h, w = 2, 16, 16
+    x0 = _bf(gen(n, cin0, h, w, seed=40))
+    x1 = _bf(gen(n, cin1, h, w, seed=41)) if cin1 else None
+    s0, t0 = bn_fold(cin0, 42)
+    cin = cin0 + cin1
+    wt = _bf(gen(cout, cin, 3, 3, seed=43, scale=0.05))
+    dy = _bf(gen(n, cout, h, w, seed=44))
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    if small:
+        a = x0
+        keep = [d(x0)]
+        srcs = [K.source(keep[0], cin0, layout=1)]
+    else:
+        a = _bf(torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)))
+        keep = [d(nhwc(x0)).bfloat16(), d(s0), d(t0)]
+        srcs = [K.source(keep[0], cin0, keep[1], keep[2])]
+        if cin1:
+            a = torch.cat((a, x1), 1)
+            keep.append(d(nhwc(x1)).bfloat16())
+            srcs.append(K.source(keep[3], cin1))
+    wr = wt.clone().requires_grad_()
+    y = F.conv2d(a, wr, padding=1)
+    (gw,) = torch.autograd.grad(y, wr, dy)
+    fwd, _, kpad = pack(wt, torch.bfloat16)
+    M = n * h * w
+    out = torch.empty(M, cout, dtype=torch.bfloat16, device=DEV)
+    ep = K.Epilogue(K.ptr(out), None, None, None, K.EP_PLAIN, 0)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 9, *srcs), K.ptr(fwd), cout, kpad, ep, K.BF16, K.stream_ptr())
+    assert rel(nchw(out.float().cpu(), n, h, w), y) < 1e-2
+    dyd = d(nhwc(dy)).bfloat16()
+    ld = K.query("selunet_wgrad_ld", 9 * cin)
+    packed = torch.zeros(cout, ld, device=DEV)
+    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs),
+           K.ptr(packed), K.BF16, K.stream_ptr())
+    gwd = torch.empty(cout, cin, 3, 3, device=DEV)
+    K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cout, cin, ld, K.ptr(gwd), K.stream_ptr())
+    assert rel(gwd.cpu(), gw) < 1e-3  # inputs exactly bf16, fp32 accumulation
+
+
+def test_convT_bf16_wgrad():
+    n, h, w, cin, cout = 2, 4, 6, 256, 128
+    x = _bf(gen(n, cin, h, w, seed=45))
+    wt = gen(cin, cout, 2, 2, seed=46, scale=0.05).requires_grad_()
+    y = F.conv_transpose2d(x, wt, stride=2)
+    dy = _bf(gen(*y.shape, seed=47))
+    (gw,) = torch.autograd.grad(y, wt, dy)
+    xd = nhwc(x).to(DEV).bfloat16()
+    dud = nhwc(dy).to(DEV).bfloat16()
+    ld = K.query("selunet_wgrad_ld", 4 * cout)
+    packed = torch.zeros(cin, ld, device=DEV)
+    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(xd, cin)), K.gather(n, h, w, 4, K.source(dud, cout)),
+           K.ptr(packed), K.BF16, K.stream_ptr())
+    gwd = torch.empty(cin, cout, 2, 2, device=DEV)
+    K.call("selunet_unpack_convT_grad", K.ptr(packed), cin, cout, K.ptr(gwd), K.stream_ptr())
+    assert rel(gwd.cpu(), gw) < 1e-3

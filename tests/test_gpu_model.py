@@ -1,0 +1,199 @@
+"""End-to-end parity of the MI355X SelectiveUNet_B training step against the reference.
+
+The expected values are the golden fixtures produced by running the reference's own model.py /
+selective_loss.py / torch Adam (tests/golden/make_golden.py). Step 0 is compared at the
+north-star tolerance (1e-4 fp32 on logits and loss, bit-exact prediction masks) and the
+gradients against the reference's own fp64 run (no worse than the reference's fp32 error);
+later steps loosely, for the reason given in tests/test_oracle.py::_run_oracle_fixture.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+import selectivenet_for_semantic_segmentation_binary_amd as S
+import selectivenet_for_semantic_segmentation_binary_amd.layout as L
+from oracle import unet_b_cpu as O
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
+from tests import _golden as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+PRE_BN_BIAS = {f"{n}.0.bias" for n, _, _ in L.CBR_LAYERS}
+
+
+def build(selective, seed=0, dtype=torch.float32):
+    net = S.UNet_B("RGB", selective=selective, compute_dtype=dtype)
+    p = L.seeded_params(seed, "RGB", selective)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    return net.to(DEV).train()
+
+
+def train_step(net, opt, x, lab, selective, lamb, chunks=1):
+    """train.py:194-209 on the MI355X path (DataParallel chunk semantics emulated in one
+    process when chunks > 1: per-chunk BN, replica-0 buffers kept, loss on the whole batch)."""
+    loss_A = S.BCEWithLogitsLoss()
+    outs, saved = [], None
+    for r, xc in enumerate(torch.chunk(x, chunks)):
+        o = net(xc)
+        outs.append(o if selective else (o,))
+        if chunks > 1 and r == 0:
+            saved = {k: v.clone() for k, v in net.named_buffers()}
+    if saved is not None:
+        with torch.no_grad():
+            for k, v in net.named_buffers():
+                v.copy_(saved[k])
+    output = torch.cat([o[0] for o in outs])
+    res = {}
+    if selective:
+        sel = torch.cat([o[1] for o in outs])
+        aux = torch.cat([o[2] for o in outs])
+        aux_loss = loss_A(aux, lab)
+        select_loss, coverage = S.calc_selective_risk_image_b(output, sel, target=lab, lamb=lamb)
+        loss = aux_loss + select_loss
+        res.update(coverage=coverage.item(), aux_loss=aux_loss.item(), select_loss=select_loss.item())
+    else:
+        loss = loss_A(output, lab)
+    opt.zero_grad()
+    loss.backward()
+    res["grads"] = {k: p.grad.detach().cpu().numpy().copy() for k, p in net.named_parameters()}
+    opt.step()
+    res.update(loss=loss.item(), output=output.detach().cpu().numpy())
+    return res
+
+
+def run_fixture(fname, strict_steps=1):
+    d = G.load(fname)
+    n, size = int(d["meta_n"]), int(d["meta_size"])
+    selective = bool(d["meta_selective"])
+    x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
+    assert hashlib.sha1(x.tobytes()).hexdigest() == d["x_sha1"].item().decode()
+    net = build(selective, int(d["meta_seed"]))
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    fails = []
+    for s in range(int(d["meta_steps"])):
+        r = train_step(net, opt, xt, lt, selective, int(d["meta_lamb"]), int(d["meta_chunks"]))
+        pre = f"s{s}/"
+        strict = s < strict_steps
+        tol = 1e-4 if strict else 1e-2
+        ref_loss = float(d[pre + "loss"])
+        assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
+        if selective:
+            assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
+        if pre + "output" in d.files:
+            assert G.max_rel(r["output"], d[pre + "output"]) < tol
+        else:
+            flat = r["output"].ravel()
+            assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol
+        if strict:
+            mask = O.train_pred_mask(r["output"])  # train.py:150,153
+            if hashlib.sha1(mask.tobytes()).hexdigest() != d[pre + "output_mask_sha1"].item().decode():
+                assert pre + "output" in d.files, "mask hash mismatch"
+                refm = O.train_pred_mask(d[pre + "output"])
+                diff = mask != refm
+                # any flipped pixel must sit within the logit tolerance of the decision boundary
+                assert np.abs(d[pre + "output"][diff]).max() < 1e-4 * np.abs(d[pre + "output"]).max(), diff.sum()
+        if s == 0:
+            # gradients: no worse than the reference's own fp32 error against its fp64 run
+            f, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
+            print(f"{fname} worst grad errors vs fp64 (ours, reference fp32):",
+                  [(n, f"{a:.1e}", f"{b:.1e}") for n, a, b in report[:6]])
+            fails += f
+            fails += G.check_tensors(d, pre + "grad", r["grads"], rtol=0.0, atol=1e-6,
+                                     skip=set(r["grads"]) - PRE_BN_BIAS)  # pre-BN biases: ~0
+        else:
+            fails += G.check_tensors(d, pre + "grad", r["grads"], rtol=0.1, atol=1e-6)
+        pv = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
+        # Adam moves an element by ~lr*sign(g); elements whose gradient sits at rounding level
+        # (pre-BN biases, near-tie ReLU/max-pool routes) can move the other way: floor 2.5*lr.
+        fails += G.check_tensors(d, pre + "param", pv, rtol=1e-5, atol=2.5e-3)
+        bufs = dict(net.named_buffers())
+        for k, v in bufs.items():
+            if "running" in k:
+                at = 1e-5 if strict else 3e-3
+                np.testing.assert_allclose(v.cpu().numpy(), d[pre + "buf/" + k], rtol=1e-4 if strict else 1e-2,
+                                           atol=at, err_msg=k)
+        assert int(bufs["encoder_layer_1_1.1.num_batches_tracked"]) == int(d[pre + "num_batches_tracked"])
+    assert not fails, "\n".join(fails[:25])
+
+
+@pytest.mark.parametrize("fname", ["step_sel_n2_64.npz", "step_nosel_n2_64.npz", "step_sel_lamb8_n3_32.npz",
+                                   "dp_sel_n8_32_c4.npz"])
+def test_train_step_matches_reference(fname):
+    run_fixture(fname)
+
+
+def test_train_step_full_size_256():
+    run_fixture("step_sel_n4_256.npz")
+
+
+def test_eval_forward_and_metrics():
+    """net.eval() forward (eval.py:156,203-205) with running statistics, eval masks (fp32 sigmoid
+    > 0.5, eval.py:175,179) and the Evaluator confusion matrix / mIoU (compute_metric.py:10-65)."""
+    d = G.load("eval_sel_n4_64.npz")
+    net = build(True)
+    with torch.no_grad():
+        for k, v in net.named_buffers():
+            if "running" in k:
+                v.copy_(torch.tensor(d["buf/" + k]))
+        for k, p in net.named_parameters():
+            if "head/" + k in d.files:
+                p.copy_(torch.tensor(d["head/" + k]))
+    net.eval()
+    with torch.no_grad():
+        o, s, a = net(torch.tensor(d["x"], device=DEV))
+    o, s = o.cpu().numpy(), s.cpu().numpy()
+    assert G.max_rel(o, d["output"]) < 1e-4 and G.max_rel(s, d["selection"]) < 1e-4
+    pred = O.eval_pred_mask(o)
+    flips = pred != d["pred"]
+    assert np.abs(d["output"][flips]).max(initial=0) < 1e-4 * np.abs(d["output"]).max()
+    if not flips.any():
+        cm = O.confusion_matrix(d["label"].astype("uint8"), pred, selection=O.eval_pred_mask(s))
+        assert np.array_equal(cm, d["eval_cm_selective"])
+        assert abs(O.miou(cm) - float(d["eval_miou_selective"])) < 0.002
+
+
+def test_bf16_step_tracks_fp32():
+    """bf16 operands / fp32 accumulation (the speed configuration): same loss to ~1e-2 and gradient
+    directions aligned with the fp32 path."""
+    d = G.load("step_sel_n2_64.npz")
+    x, lab = make_batch(2, 64, seed=int(d["meta_data_seed"]))
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    res = {}
+    for dt in (torch.float32, torch.bfloat16):
+        net = build(True, dtype=dt)
+        opt = S.Adam(net.parameters(), lr=1e-3)
+        res[dt] = train_step(net, opt, xt, lt, True, 2)
+    a, b = res[torch.float32], res[torch.bfloat16]
+    assert abs(a["loss"] - b["loss"]) < 2e-2 * abs(a["loss"])
+    for k in a["grads"]:
+        if k in PRE_BN_BIAS:
+            continue
+        ga, gb = a["grads"][k].ravel().astype(np.float64), b["grads"][k].ravel().astype(np.float64)
+        cos = ga @ gb / (np.linalg.norm(ga) * np.linalg.norm(gb) + 1e-30)
+        assert cos > 0.9, (k, cos)
+
+
+def test_adam_matches_reference_algorithm():
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV) for n in (5, 4096, 10000)]
+    ref = [p.detach().cpu().clone().requires_grad_() for p in ps]
+    params = [torch.nn.Parameter(p.clone()) for p in ps]
+    opt = S.Adam(params, lr=1e-2, weight_decay=0.01)
+    ropt = torch.optim.Adam(ref, lr=1e-2, weight_decay=0.01)
+    for step in range(3):
+        for p, r in zip(params, ref):
+            g = torch.randn(p.shape) * (step + 1)
+            p.grad = g.to(DEV)
+            r.grad = g.clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(params, ref):
+        assert torch.allclose(p.detach().cpu(), r.detach(), rtol=1e-6, atol=1e-6)
+    sd = opt.state_dict()
+    ropt2 = torch.optim.Adam([r.detach().clone().requires_grad_() for r in ref], lr=1e-2)
+    ropt2.load_state_dict(sd)  # checkpoint interchangeability (utils/net_utils.py:5-9)
