@@ -74,8 +74,8 @@ enum { SELUNET_EP_PLAIN = 0, SELUNET_EP_SPLIT = 1, SELUNET_EP_SCATTER2X = 2 };
  * out0[M][split], the rest to out1[M][N-split] (backward of torch.cat); SCATTER2X:
  * column (a*2+b)*Cq + c of row (img,y,x) goes to out0[img][2y+a][2x+b][c], Cq = N/4
  * (ConvTranspose2d k2 s2 forward). bias (fp32, per output channel) is added when
- * non-NULL. stats (fp32 [ceil(M/128)][2][N]): per-workgroup column sum and sum of
- * squares of the fp32 accumulators (BatchNorm batch statistics, model.py:12). */
+ * non-NULL. stats (fp32 [selunet_gemm_stats_rows(a, N, dtype)][2][N]): per-workgroup column
+ * sum and sum of squares of the fp32 accumulators (BatchNorm batch statistics, model.py:12). */
 typedef struct selunet_epilogue {
   void* out0;
   void* out1;
@@ -107,6 +107,9 @@ int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float
  * data-gradient, conv_transpose2d forward and data-gradient (model.py:11,44,51,57). */
 int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
                         const selunet_epilogue* ep, int32_t dtype, void* stream);
+/* Rows of the stats slab selunet_gemm_gather writes for this operand (pixel tiles of the
+ * kernel it dispatches to: 16x16 halo tiles for 3x3 taps, else 128-row tiles); -1 on error. */
+int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t dtype);
 /* out[ni][nj] += sum_m G_p[m][i] * G_q[m][j] (fp32 atomics; out zeroed by the caller).
  * Replaces the weight-gradient of conv2d / conv_transpose2d (train.py:208 backward). */
 int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out,
@@ -149,6 +152,12 @@ int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const 
 int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
                          const float* shift, const float* mean, const float* invstd,
                          const float* coef, void* dy, int32_t dtype, void* stream);
+
+/* ---- first layer (C_in = 3 or 2, model.py:24-29) --------------------------------------- */
+/* x NCHW fp32 -> out [n*h*w][k_pad] in dtype: column tap*c + ci of the 3x3 pad-1 window, zero
+ * for columns >= 9c. The first conv then runs as selunet_gemm_gather with taps = 1. */
+int selunet_im2col3x3(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, int32_t k_pad, void* out,
+                      int32_t dtype, void* stream);
 
 /* ---- MaxPool2d(2) on relu(bn(y)) (model.py:31,35,39) ---------------------------------- */
 int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,

@@ -56,6 +56,7 @@ SIGNATURES = {
                                       c_int32, P]),
     "selunet_gemm_wgrad": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int32, P]),
     "selunet_wgrad_ld": (c_int32, [c_int32]),
+    "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_reduce_ws_bytes": (c_int64, [c_int32]),
     "selunet_reduce_rows": (c_int32, [P, c_int64, c_int32, P, P, P, P]),
     "selunet_channel_slab_rows": (c_int64, [c_int64]),
@@ -65,6 +66,7 @@ SIGNATURES = {
     "selunet_bn_bwd_reduce": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_finalize": (c_int32, [P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
+    "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),
     "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
     "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, c_int32, P]),
     "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),

@@ -1,0 +1,418 @@
+// 3x3 / stride 1 / pad 1 convolution (model.py:11) as an MFMA implicit GEMM whose A operand is
+// staged once per channel chunk as a (16+2) x (16+2)-pixel halo tile in LDS: the nine taps read
+// shifted 16x16 windows of the same tile instead of re-gathering every input pixel nine times
+// through L2. Used for the conv forward (BN+ReLU of the producer folded into the staging, torch.cat
+// sources read in place) and for the data-gradient (dY with the flipped/transposed weight pack).
+//
+// Workgroup: 512 threads = 8 waves (2 per SIMD), output tile 16x16 pixels x BN channels
+// (BN = 128: waves 4(M) x 2(N), 64 px x 64 ch each; BN = 64: 8 x 1, 32 px x 64 ch). One K-step =
+// one tap x one 128-B channel chunk (32 fp32 / 64 bf16 channels). B (weights) is double-buffered
+// per step; the next chunk's halo is loaded a 16-B slice per thread per tap during the current
+// chunk's first six taps (load early, write late) into the second halo buffer.
+// LDS rows are 144 B (128 B + 16 B pad) so ds_read_b128 fragment reads of 16 consecutive rows hit
+// 16 distinct bank slots.
+#include "gemm_common.h"
+
+namespace selunet {
+
+constexpr int TH = 16, TW = 16;         // output tile (pixels)
+constexpr int HHT = TH + 2, HWT = TW + 2;  // halo tile
+constexpr int HPIX = HHT * HWT;         // 324 halo pixels
+constexpr int HTHREADS = 512;
+constexpr int A_ROUNDS = (HPIX * 8 + HTHREADS - 1) / HTHREADS;  // 16-B halo loads per thread per chunk
+
+template <typename T, int BN>
+__global__ void __launch_bounds__(HTHREADS, 2)
+conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int tiles_x,
+                    int tiles_y) {
+  constexpr int E = 16 / sizeof(T);       // elements per 16-B vector
+  constexpr int CK = 128 / sizeof(T);     // channels per chunk
+  constexpr int WAVES_N = BN / 64;
+  constexpr int WAVES_M = 8 / WAVES_N;
+  constexpr int WPIX = (TH * TW) / WAVES_M;  // 64 or 32 pixels per wave
+  constexpr int MT = WPIX / 32;
+  constexpr int NT = 2;                   // 64 channels per wave
+  constexpr int B_ROUNDS = (BN * 8 + HTHREADS - 1) / HTHREADS;
+
+  constexpr int SMEM_MAIN = 2 * HPIX * ROWB + 2 * BN * ROWB, SMEM_EPI = TH * TW * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + 2 * HPIX * ROWB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const int n_tile = blockIdx.x % n_tiles;
+  const int ptile = blockIdx.x / n_tiles;
+  const int tx_t = ptile % tiles_x;
+  const int rest = ptile / tiles_x;
+  const int ty_t = rest % tiles_y;
+  const int img = rest / tiles_y;
+  const int y0 = ty_t * TH, x0 = tx_t * TW;
+  const int n0 = n_tile * BN;
+
+  const int nchunks = g.Ctot / CK;
+  const int nsteps = nchunks * 9;
+
+  // ---------------------------------------------------------------- staging helpers
+  uint4 ra;
+  bool aok;
+  int a_s = 0, a_c = 0;
+  auto a_load = [&](int chunk, int round) {
+    const int hidx = round * HTHREADS + tid;
+    aok = false;
+    ra = make_uint4(0, 0, 0, 0);
+    if (hidx >= HPIX * 8) return;
+    const int hp = hidx >> 3, cc = hidx & 7;
+    const int hy = hp / HWT, hx = hp - hy * HWT;
+    const int ys = y0 - 1 + hy, xs = x0 - 1 + hx;
+    int c = chunk * CK;
+    int s = 0;
+    if (g.nsrc > 1 && c >= g.src[0].C) {
+      c -= g.src[0].C;
+      s = 1;
+    }
+    a_s = s;
+    a_c = c + cc * E;
+    if ((unsigned)ys < (unsigned)g.h && (unsigned)xs < (unsigned)g.w) {
+      const SrcArg& sa = g.src[s];
+      ra = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
+                                          (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + a_c);
+      aok = true;
+    }
+  };
+  auto a_store = [&](int buf, int round) {
+    const int hidx = round * HTHREADS + tid;
+    if (hidx >= HPIX * 8) return;
+    const int hp = hidx >> 3, cc = hidx & 7;
+    const SrcArg& sa = g.src[a_s];
+    uint4 v = ra;
+    if (sa.scale) v = aok ? transform16<T>(v, sa.scale, sa.shift, a_c, sa.relu) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(As + (buf * HPIX + hp) * ROWB + cc * 16) = v;
+  };
+  uint4 rb[B_ROUNDS];
+  auto b_load = [&](int step) {
+    const int chunk = step / 9, tap = step - chunk * 9;
+    const int k0 = tap * g.Ctot + chunk * CK;
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      if (row < BN) rb[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
+    }
+  };
+  auto b_store = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      if (row < BN) *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb[r];
+    }
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  // per-lane halo row of pixel (subtile a, lane) for tap (0,0)
+  int hrow0[MT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+    const int pix = wm * WPIX + a * 32 + l32;
+    hrow0[a] = (pix / TW) * HWT + (pix % TW);
+  }
+
+  // ---------------------------------------------------------------- prologue
+  for (int r = 0; r < A_ROUNDS; ++r) {
+    a_load(0, r);
+    a_store(0, r);
+  }
+  b_load(0);
+  b_store(0);
+  __syncthreads();
+
+  // ---------------------------------------------------------------- main loop
+  for (int s = 0; s < nsteps; ++s) {
+    const int c = s / 9, t = s - (s / 9) * 9;
+    const bool more_b = s + 1 < nsteps;
+    const bool do_a = (c + 1 < nchunks) && (t < A_ROUNDS);
+    if (more_b) b_load(s + 1);
+    if (do_a) a_load(c + 1, t);
+
+    const unsigned char* a_src = As + (c & 1) * HPIX * ROWB;
+    const unsigned char* b_src = Bs + (s & 1) * BN * ROWB;
+    const int dy = t / 3, dx = t - (t / 3) * 3;
+    const int tap_off = dy * HWT + dx;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int boff = q * 32 + half * 16;
+      uint4 af[MT], bfr[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * ROWB + boff);
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+    }
+    if (more_b) b_store((s + 1) & 1);
+    if (do_a) a_store((c + 1) & 1, t);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue (LDS-staged)
+  float* tile = reinterpret_cast<float*>(smem);  // [256][BN + 4]; the loop ended with a barrier
+  acc_to_lds<MT, NT, BN>(tile, acc, wm * WPIX, wn * 64, lane);
+  __syncthreads();
+  auto dst = [&](int pix, int c) -> T* {
+    const int y = y0 + pix / TW, x = x0 + pix % TW;
+    if (y >= g.h || x >= g.w) return nullptr;
+    const int64_t m = ((int64_t)img * g.h + y) * g.w + x;
+    const int col = n0 + c;
+    if (ep.mode == SELUNET_EP_SPLIT)
+      return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                            : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+    return reinterpret_cast<T*>(ep.out0) + m * N + col;
+  };
+  auto bias_col = [&](int c) { return n0 + c; };
+  float* st = ep.stats ? ep.stats + ((int64_t)ptile * 2) * N + n0 : nullptr;
+  lds_tile_store<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, st, N);
+}
+
+// =========================================================================== weight gradient
+// dW[co][tap][ci] = sum_p dY[p][co] * X[p + off(tap)][ci] for one co tile (BI) and one 64-channel
+// ci chunk, reduced over the pixel tiles (8 x 16) of a split; fp32 atomics at the end.
+// Each pixel tile stages dY [128 px][BI] and the input halo [10 x 18 px][64 ch] in LDS in their
+// natural layouts; the MFMA k dimension is the pixel, so both operands are read with
+// ds_read_b64_tr_b16 (4 pixels x 16 channels per 16-lane group). One dY fragment feeds the MFMAs
+// of every tap the wave owns. 8 waves: (BI/32 co subtiles) x (2 ci subtiles) x (taps split in two
+// groups when BI = 64). Rows are padded to a stride of 16 dwords mod 64 so the transposed reads
+// of 4 consecutive rows hit distinct banks.
+constexpr int WTH = 8, WTW = 16;                 // pixel tile
+constexpr int WHH = WTH + 2, WHW = WTW + 2;      // halo
+constexpr int WHP = WHH * WHW;                   // 180 halo pixels
+constexpr int WPIXT = WTH * WTW;                 // 128 pixels
+
+template <int BI>
+__global__ void __launch_bounds__(512, 2)
+conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int co_tiles, int ci_chunks,
+                          int64_t tiles_per_split, int tiles_x, int tiles_y, int64_t total_tiles) {
+  constexpr int LDP = BI + 32;                   // dY tile row stride (elements)
+  constexpr int LDX = 64 + 32;                   // halo row stride (elements)
+  constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
+  constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
+  constexpr int P_ROUNDS = (WPIXT * BI / 8) / 512;
+  constexpr int X_ROUNDS = (WHP * 8 + 511) / 512;
+
+  __shared__ __attribute__((aligned(16))) unsigned short Ps[2][WPIXT][LDP];
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[2][WHP][LDX];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wj = wave & 1;                       // ci subtile
+  const int wi = (wave >> 1) % (BI / 32);        // co subtile
+  const int tg = (wave >> 1) / (BI / 32);        // tap group
+  const int tap0 = tg * 5;
+  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
+  const int half = lane >> 5, l32 = lane & 31;
+  const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  const int cot = blockIdx.x % co_tiles;
+  const int rest = blockIdx.x / co_tiles;
+  const int cik = rest % ci_chunks;
+  const int64_t split = rest / ci_chunks;
+  const int i0 = cot * BI;
+  const int c0 = cik * 64;
+  const int64_t pt_begin = split * tiles_per_split;
+  const int64_t pt_end = min(total_tiles, pt_begin + tiles_per_split);
+  if (pt_begin >= pt_end) return;
+
+  // source of this ci chunk
+  int xs_src = 0, xc = c0;
+  if (Q.nsrc > 1 && xc >= Q.src[0].C) {
+    xc -= Q.src[0].C;
+    xs_src = 1;
+  }
+  const SrcArg& xa = Q.src[xs_src];
+  const SrcArg& pa = P.src[0];
+  const int H = P.h, W = P.w;
+
+  uint4 rp[P_ROUNDS], rx[X_ROUNDS];
+  bool xok[X_ROUNDS];
+  auto load_tile = [&](int64_t pt) {
+    const int tx = (int)(pt % tiles_x);
+    const int64_t r2 = pt / tiles_x;
+    const int ty = (int)(r2 % tiles_y);
+    const int img = (int)(r2 / tiles_y);
+    const int y0 = ty * WTH, x0 = tx * WTW;
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 8), cc = idx % (BI / 8);
+      const int y = y0 + px / WTW, x = x0 + px % WTW;
+      rp[r] = make_uint4(0, 0, 0, 0);
+      if (y < H && x < W) {
+        const int c = i0 + cc * 8;
+        rp[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(pa.data) +
+                                               (((int64_t)img * H + y) * W + x) * pa.C + c);
+        if (pa.scale) rp[r] = transform16<__bf16>(rp[r], pa.scale, pa.shift, c, pa.relu);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      rx[r] = make_uint4(0, 0, 0, 0);
+      xok[r] = false;
+      if (idx < WHP * 8) {
+        const int hp = idx >> 3, cc = idx & 7;
+        const int y = y0 - 1 + hp / WHW, x = x0 - 1 + hp % WHW;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+          rx[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(xa.data) +
+                                                 (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 8);
+          xok[r] = true;
+        }
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 8), cc = idx % (BI / 8);
+      *reinterpret_cast<uint4*>(&Ps[buf][px][cc * 8]) = rp[r];
+    }
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      if (idx < WHP * 8) {
+        const int hp = idx >> 3, cc = idx & 7;
+        uint4 v = rx[r];
+        if (xa.scale) v = xok[r] ? transform16<__bf16>(v, xa.scale, xa.shift, xc + cc * 8, xa.relu)
+                                 : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(&Xs[buf][hp][cc * 8]) = v;
+      }
+    }
+  };
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
+
+  load_tile(pt_begin);
+  store_tile(0);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t pt = pt_begin; pt < pt_end; ++pt) {
+    const bool more = pt + 1 < pt_end;
+    if (more) load_tile(pt + 1);
+#pragma unroll
+    for (int ks = 0; ks < WTH; ++ks) {   // one tile row (16 pixels) per k-step
+      const int prow = ks * WTW + 8 * half + q4;
+      const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow][pcol]);
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow + 4][pcol]);
+      const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      const int xcol = wj * 32 + 16 * grp_hi + 4 * p4;
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t) {
+        if (t < ntap) {
+          const int tap = tap0 + t;
+          const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+          const int xrow = (ks + dy) * WHW + 8 * half + dx + q4;
+          s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow][xcol]);
+          s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow + 4][xcol]);
+          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_tile(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  const int ctot = Q.Ctot;
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) {
+    if (t < ntap) {
+      const int tap = tap0 + t;
+      const int j = tap * ctot + c0 + wj * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        atomicAdd(out + (int64_t)i * ldo + j, acc[t][r]);
+      }
+    }
+  }
+}
+
+bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype) {
+  if (dtype != SELUNET_BF16) return false;
+  if (p.taps != 1 || p.nsrc != 1 || p.small || p.src[0].layout != 0 || p.K % 64 != 0) return false;
+  if (q.taps != 9 || q.small || q.h < 8 || q.w < 16) return false;
+  for (int s = 0; s < q.nsrc; ++s)
+    if (q.src[s].C % 64 != 0 || q.src[s].layout != 0) return false;
+  return true;
+}
+
+int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, hipStream_t st) {
+  const int ni = p.K;
+  const int bi = ni % 128 == 0 ? 128 : 64;
+  const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
+  const int tiles_x = (int)cdiv(q.w, WTW), tiles_y = (int)cdiv(q.h, WTH);
+  const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
+  const int64_t want = std::max<int64_t>(1, cdiv(512, (int64_t)co_tiles * ci_chunks));
+  const int64_t per = cdiv(total, std::min(total, want));
+  const int64_t splits = cdiv(total, per);
+  const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
+  if (bi == 128)
+    hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
+                       ci_chunks, per, tiles_x, tiles_y, total);
+  else
+    hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<64>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
+                       ci_chunks, per, tiles_x, tiles_y, total);
+  return check_launch("conv3x3_wgrad_halo");
+}
+
+bool conv3x3_halo_eligible(const GatherArg& g, int N, int dtype) {
+  const int ck = dtype == SELUNET_F32 ? 32 : 64;
+  if (g.taps != 9 || g.small || g.h < 16 || g.w < 16) return false;
+  if (g.Ctot % ck != 0 || (g.nsrc > 1 && g.src[0].C % ck != 0)) return false;
+  for (int s = 0; s < g.nsrc; ++s)
+    if (g.src[s].layout != 0) return false;
+  return N % 64 == 0;
+}
+
+int64_t conv3x3_halo_tiles(const GatherArg& g) {
+  return (int64_t)g.n * cdiv(g.h, TH) * cdiv(g.w, TW);
+}
+
+template <typename T, int BN>
+static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
+  const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
+  const int n_tiles = N / BN;
+  const int64_t blocks = conv3x3_halo_tiles(g) * n_tiles;
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, BN>), dim3((unsigned)blocks), dim3(HTHREADS), 0, st, g,
+                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y);
+}
+
+int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
+                        hipStream_t st) {
+  const bool bn128 = N % 128 == 0 && !(ep.mode == SELUNET_EP_SPLIT && ep.split % 128 != 0);
+  if (dtype == SELUNET_F32) {
+    if (bn128) launch_halo<float, 128>(g, b, N, k_pad, ep, st);
+    else launch_halo<float, 64>(g, b, N, k_pad, ep, st);
+  } else {
+    if (bn128) launch_halo<__bf16, 128>(g, b, N, k_pad, ep, st);
+    else launch_halo<__bf16, 64>(g, b, N, k_pad, ep, st);
+  }
+  return check_launch("conv3x3_halo");
+}
+
+}  // namespace selunet

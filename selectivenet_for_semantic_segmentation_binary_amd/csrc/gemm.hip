@@ -19,138 +19,9 @@
 //  bf16: v_mfma_f32_32x32x16_bf16; a 16-B fragment is the 8 k's of one half-wave.
 #include <type_traits>
 
-#include "common.h"
+#include "gemm_common.h"
 
 namespace selunet {
-
-struct SrcArg {
-  const void* data;
-  const float* scale;
-  const float* shift;
-  int C;
-  int relu;
-  int layout;
-  int pad;
-};
-
-struct GatherArg {
-  int n, h, w;       // row grid
-  int taps;          // 1, 4, 9
-  int nsrc;
-  int Ctot;          // C0 + C1
-  int hs, ws;        // source grid
-  int K;             // taps * Ctot (true K)
-  int small;         // element-wise gather (channels not a multiple of the staging vector)
-  int64_t M;
-  SrcArg src[2];
-};
-
-constexpr int BM = SELUNET_GEMM_BM;
-constexpr int ROWB = 144;  // padded LDS row bytes for a 128-B K slice
-
-// --------------------------------------------------------------------------- gather helpers
-__device__ inline void tap_offset(int taps, int tap, int& dy, int& dx) {
-  if (taps == 9) {
-    dy = tap / 3 - 1;
-    dx = tap - (tap / 3) * 3 - 1;
-  } else if (taps == 4) {
-    dy = tap >> 1;
-    dx = tap & 1;
-  } else {
-    dy = 0;
-    dx = 0;
-  }
-}
-
-// source pixel of row pixel (y, x) for `tap`; returns false when it falls into the zero pad.
-__device__ inline bool src_pixel(const GatherArg& g, int tap, int y, int x, int& ys, int& xs) {
-  int dy, dx;
-  tap_offset(g.taps, tap, dy, dx);
-  if (g.taps == 4) {
-    ys = 2 * y + dy;
-    xs = 2 * x + dx;
-    return true;
-  }
-  ys = y + dy;
-  xs = x + dx;
-  return (unsigned)ys < (unsigned)g.hs && (unsigned)xs < (unsigned)g.ws;
-}
-
-// One gathered element (slow path, small C / non-vector channel counts). Applies the transform.
-template <typename T>
-__device__ inline float gather_scalar(const GatherArg& g, int64_t m, int k) {
-  if (m >= g.M || k >= g.K) return 0.0f;
-  const int tap = k / g.Ctot;
-  int c = k - tap * g.Ctot;
-  int s = 0;
-  if (g.nsrc > 1 && c >= g.src[0].C) {
-    c -= g.src[0].C;
-    s = 1;
-  }
-  const int x = (int)(m % g.w);
-  const int64_t t = m / g.w;
-  const int y = (int)(t % g.h);
-  const int img = (int)(t / g.h);
-  int ys, xs;
-  if (!src_pixel(g, tap, y, x, ys, xs)) return 0.0f;
-  const SrcArg& sa = g.src[s];
-  float v;
-  if (sa.layout == 1) {
-    v = reinterpret_cast<const float*>(sa.data)[(((int64_t)img * sa.C + c) * g.hs + ys) * g.ws + xs];
-  } else {
-    v = to_f(reinterpret_cast<const T*>(sa.data)[(((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c]);
-  }
-  if (sa.scale) {
-    v = v * sa.scale[c] + sa.shift[c];
-    if (sa.relu) v = fmaxf(v, 0.0f);
-  }
-  return v;
-}
-
-// --------------------------------------------------------------------------- MFMA wrappers
-template <typename T> struct Mma;
-template <> struct Mma<float> {
-  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-  }
-};
-template <> struct Mma<__bf16> {
-  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
-    bf16x8 av = __builtin_bit_cast(bf16x8, a);
-    bf16x8 bv = __builtin_bit_cast(bf16x8, b);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
-  }
-};
-
-// apply folded BN + ReLU to a 16-B vector of T (E elements), channel base c
-template <typename T>
-__device__ inline uint4 transform16(uint4 raw, const float* scale, const float* shift, int c, int relu) {
-  constexpr int E = 16 / sizeof(T);
-  T v[E];
-  __builtin_memcpy(v, &raw, 16);
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    float f = to_f(v[e]) * scale[c + e] + shift[c + e];
-    if (relu) f = fmaxf(f, 0.0f);
-    v[e] = from_f<T>(f);
-  }
-  uint4 out;
-  __builtin_memcpy(&out, v, 16);
-  return out;
-}
-
-// =========================================================================== gemm_gather
-struct EpiArg {
-  void* out0;
-  void* out1;
-  const float* bias;
-  float* stats;
-  int mode;
-  int split;
-};
 
 template <typename T, int BN>
 __global__ void __launch_bounds__(256, 2)
@@ -163,7 +34,8 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   constexpr int AR = BM / 32;                // A rows staged per thread
   constexpr int BR = BN / 32;                // B rows staged per thread
 
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * ROWB];
+  constexpr int SMEM_MAIN = 2 * (BM + BN) * ROWB, SMEM_EPI = BM * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
   unsigned char* As = smem;                          // [2][BM][ROWB]
   unsigned char* Bs = smem + 2 * BM * ROWB;          // [2][BN][ROWB]
 
@@ -295,74 +167,30 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     __syncthreads();
   }
 
-  // ------------------------------------------------------------------ epilogue
+  // ------------------------------------------------------------------ epilogue (LDS-staged)
+  float* tile = reinterpret_cast<float*>(smem);  // [BM][BN + 4]; the loop ended with a barrier
+  acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
+  __syncthreads();
   const int Cq = N >> 2;
-#pragma unroll
-  for (int a = 0; a < MT; ++a) {
-#pragma unroll
-    for (int b = 0; b < NT; ++b) {
-      const int col = n0 + wn * WN + b * 32 + l32;
-      float bias = 0.0f;
-      if (ep.bias) bias = ep.bias[ep.mode == SELUNET_EP_SCATTER2X ? (col % Cq) : col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        const int64_t m = m0 + row;
-        if (m >= g.M) continue;
-        const float v = acc[a][b][r] + bias;
-        if (ep.mode == SELUNET_EP_PLAIN) {
-          reinterpret_cast<T*>(ep.out0)[m * N + col] = from_f<T>(v);
-        } else if (ep.mode == SELUNET_EP_SPLIT) {
-          if (col < ep.split)
-            reinterpret_cast<T*>(ep.out0)[m * ep.split + col] = from_f<T>(v);
-          else
-            reinterpret_cast<T*>(ep.out1)[m * (N - ep.split) + (col - ep.split)] = from_f<T>(v);
-        } else {
-          const int ab = col / Cq, c = col - ab * Cq;
-          const int x = (int)(m % g.w);
-          const int64_t t = m / g.w;
-          const int y = (int)(t % g.h);
-          const int64_t img = t / g.h;
-          const int64_t o = ((img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + c;
-          reinterpret_cast<T*>(ep.out0)[o] = from_f<T>(v);
-        }
-      }
-    }
-  }
-
-  if (ep.stats) {
-    // column sum / sum of squares over this workgroup's valid rows (fp32 accumulators)
-    float* red = reinterpret_cast<float*>(smem);  // [2][BN][2], LDS free after the final barrier
-#pragma unroll
-    for (int b = 0; b < NT; ++b) {
-      float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll
-      for (int a = 0; a < MT; ++a)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          if (m0 + row < g.M) {
-            const float v = acc[a][b][r];
-            s1 += v;
-            s2 += v * v;
-          }
-        }
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (half == 0) {
-        const int col = wn * WN + b * 32 + l32;
-        red[(wm * BN + col) * 2 + 0] = s1;
-        red[(wm * BN + col) * 2 + 1] = s2;
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const float s1 = red[(0 * BN + tid) * 2 + 0] + red[(1 * BN + tid) * 2 + 0];
-      const float s2 = red[(0 * BN + tid) * 2 + 1] + red[(1 * BN + tid) * 2 + 1];
-      ep.stats[(m_tile * 2 + 0) * N + n0 + tid] = s1;
-      ep.stats[(m_tile * 2 + 1) * N + n0 + tid] = s2;
-    }
-  }
+  auto dst = [&](int row, int c) -> T* {
+    const int64_t m = m0 + row;
+    if (m >= g.M) return nullptr;
+    const int col = n0 + c;
+    if (ep.mode == SELUNET_EP_PLAIN) return reinterpret_cast<T*>(ep.out0) + m * N + col;
+    if (ep.mode == SELUNET_EP_SPLIT)
+      return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                            : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+    const int ab = col / Cq, cq = col - ab * Cq;
+    const int x = (int)(m % g.w);
+    const int64_t t = m / g.w;
+    const int y = (int)(t % g.h);
+    const int64_t img = t / g.h;
+    return reinterpret_cast<T*>(ep.out0) +
+           ((img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + cq;
+  };
+  auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
+  float* st = ep.stats ? ep.stats + (m_tile * 2) * N + n0 : nullptr;
+  lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, st, N);
 }
 
 // =========================================================================== gemm_wgrad
@@ -511,7 +339,6 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
 // and hands lane j column j's 4 values, so two reads give lane (col = l & 31, half = l >> 5)
 // the k-run m = 8*half .. 8*half+7 of its column. Rows are padded by 64 B so the 32 lanes of a
 // read touch 64 distinct banks (row stride = 16 dwords mod 64).
-typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ inline uint4 gather_vec8_bf16(const GatherArg& g, int64_t m, int k, int tap, int s, int c, bool vec,
                                          bool in) {
@@ -662,7 +489,7 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
 }
 
 // =========================================================================== host side
-static int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems) {
+int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems) {
   SELUNET_REQUIRE(a != nullptr, "gather descriptor is NULL");
   SELUNET_REQUIRE(a->n > 0 && a->h > 0 && a->w > 0, "gather grid must be positive (%d,%d,%d)", a->n, a->h, a->w);
   SELUNET_REQUIRE(a->taps == 1 || a->taps == 4 || a->taps == 9, "taps must be 1, 4 or 9 (got %d)", a->taps);
@@ -734,6 +561,22 @@ static void launch_wgrad(const GatherArg& p, const GatherArg& q, float* out, int
 
 using namespace selunet;
 
+bool selunet::halo_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("SELUNET_NO_HALO");
+    return !(v && v[0] == '1');
+  }();
+  return on;
+}
+
+extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t dtype) {
+  const int esz = dtype == SELUNET_F32 ? 4 : 2;
+  GatherArg g;
+  if (make_gather(a, dtype, g, 16 / esz)) return -1;
+  if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_tiles(g);
+  return cdiv(g.M, BM);
+}
+
 extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
                                    const selunet_epilogue* ep, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
@@ -756,6 +599,8 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
   SELUNET_REQUIRE(ep->stats == nullptr || ep->mode == SELUNET_EP_PLAIN, "stats only with the plain epilogue");
   EpiArg e{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split};
   hipStream_t st = as_stream(stream);
+  if (ep->mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype))
+    return conv3x3_halo_launch(g, b, n_cols, k_pad, e, dtype, st);
   const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
   if (dtype == SELUNET_F32) {
     if (bn128) launch_gather<float, 128>(g, b, n_cols, k_pad, e, st);
@@ -782,6 +627,8 @@ extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather*
   const int bj = (gq.K % 128 == 0 || gq.K > 512) ? 128 : 64;
   const int nj_pad = (int)(cdiv(gq.K, bj) * bj);
   hipStream_t st = as_stream(stream);
+  if (halo_enabled() && conv3x3_wgrad_halo_eligible(gp, gq, dtype))
+    return conv3x3_wgrad_halo_launch(gp, gq, out, nj_pad, st);
   const bool bi128 = ni % 128 == 0;
   // out is [ni][nj_pad] where nj_pad = roundup(Kq, 64 or 128): see selunet_wgrad_ld()
   if (dtype == SELUNET_F32) {

@@ -1,0 +1,232 @@
+// Device-side operand descriptors and helpers shared by the implicit-GEMM kernels.
+#pragma once
+
+#include "common.h"
+
+namespace selunet {
+
+struct SrcArg {
+  const void* data;
+  const float* scale;
+  const float* shift;
+  int C;
+  int relu;
+  int layout;
+  int pad;
+};
+
+struct GatherArg {
+  int n, h, w;       // row grid
+  int taps;          // 1, 4, 9
+  int nsrc;
+  int Ctot;          // C0 + C1
+  int hs, ws;        // source grid
+  int K;             // taps * Ctot (true K)
+  int small;         // element-wise gather (channels not a multiple of the staging vector)
+  int64_t M;
+  SrcArg src[2];
+};
+
+constexpr int BM = SELUNET_GEMM_BM;
+constexpr int ROWB = 144;  // padded LDS row bytes for a 128-B K slice
+
+// --------------------------------------------------------------------------- gather helpers
+__device__ inline void tap_offset(int taps, int tap, int& dy, int& dx) {
+  if (taps == 9) {
+    dy = tap / 3 - 1;
+    dx = tap - (tap / 3) * 3 - 1;
+  } else if (taps == 4) {
+    dy = tap >> 1;
+    dx = tap & 1;
+  } else {
+    dy = 0;
+    dx = 0;
+  }
+}
+
+// source pixel of row pixel (y, x) for `tap`; returns false when it falls into the zero pad.
+__device__ inline bool src_pixel(const GatherArg& g, int tap, int y, int x, int& ys, int& xs) {
+  int dy, dx;
+  tap_offset(g.taps, tap, dy, dx);
+  if (g.taps == 4) {
+    ys = 2 * y + dy;
+    xs = 2 * x + dx;
+    return true;
+  }
+  ys = y + dy;
+  xs = x + dx;
+  return (unsigned)ys < (unsigned)g.hs && (unsigned)xs < (unsigned)g.ws;
+}
+
+// One gathered element (slow path, small C / non-vector channel counts). Applies the transform.
+template <typename T>
+__device__ inline float gather_scalar(const GatherArg& g, int64_t m, int k) {
+  if (m >= g.M || k >= g.K) return 0.0f;
+  const int tap = k / g.Ctot;
+  int c = k - tap * g.Ctot;
+  int s = 0;
+  if (g.nsrc > 1 && c >= g.src[0].C) {
+    c -= g.src[0].C;
+    s = 1;
+  }
+  const int x = (int)(m % g.w);
+  const int64_t t = m / g.w;
+  const int y = (int)(t % g.h);
+  const int img = (int)(t / g.h);
+  int ys, xs;
+  if (!src_pixel(g, tap, y, x, ys, xs)) return 0.0f;
+  const SrcArg& sa = g.src[s];
+  float v;
+  if (sa.layout == 1) {
+    v = reinterpret_cast<const float*>(sa.data)[(((int64_t)img * sa.C + c) * g.hs + ys) * g.ws + xs];
+  } else {
+    v = to_f(reinterpret_cast<const T*>(sa.data)[(((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c]);
+  }
+  if (sa.scale) {
+    v = v * sa.scale[c] + sa.shift[c];
+    if (sa.relu) v = fmaxf(v, 0.0f);
+  }
+  return v;
+}
+
+// --------------------------------------------------------------------------- MFMA wrappers
+template <typename T> struct Mma;
+template <> struct Mma<float> {
+  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<__bf16> {
+  __device__ static inline void run(f32x16& acc, uint4 a, uint4 b) {
+    bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    bf16x8 bv = __builtin_bit_cast(bf16x8, b);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+  }
+};
+
+// apply folded BN + ReLU to a 16-B vector of T (E elements), channel base c
+template <typename T>
+__device__ inline uint4 transform16(uint4 raw, const float* scale, const float* shift, int c, int relu) {
+  constexpr int E = 16 / sizeof(T);
+  T v[E];
+  __builtin_memcpy(v, &raw, 16);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float f = to_f(v[e]) * scale[c + e] + shift[c + e];
+    if (relu) f = fmaxf(f, 0.0f);
+    v[e] = from_f<T>(f);
+  }
+  uint4 out;
+  __builtin_memcpy(&out, v, 16);
+  return out;
+}
+
+// =========================================================================== gemm_gather
+struct EpiArg {
+  void* out0;
+  void* out1;
+  const float* bias;
+  float* stats;
+  int mode;
+  int split;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// --------------------------------------------------------------------------- LDS-staged epilogue
+// Accumulators of the wave's MT x NT 32x32 subtiles (tile coords (wr0 + a*32, wc0 + b*32)) ->
+// fp32 LDS tile [TR][TC + 4]. C/D layout of the 32x32 MFMAs: col = lane & 31,
+// row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+template <int MT, int NT, int TC>
+__device__ inline void acc_to_lds(float* tile, const f32x16 (&acc)[MT][NT], int wr0, int wc0, int lane) {
+  const int half = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        tile[(wr0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * (TC + 4) + wc0 + b * 32 + l32] = acc[a][b][r];
+}
+
+// Store the LDS tile as 8-column vectors (16 B bf16 / 32 B fp32): dst(row, col) returns the
+// global address of tile element (row, col) (col a multiple of 8) or nullptr for a masked row.
+// bias (nullable) is indexed by bias_col(col). If stats != nullptr, per-column sum / sum of
+// squares over the stored rows (before the bias) go to stats[0][col], stats[1][col] of the
+// block's slab row (stride ld_stats between the two).
+template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
+__device__ inline void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
+                                      float* stats, int ld_stats) {
+  constexpr int CC = TC / 8;            // 8-column chunks per row
+  constexpr int RS = NTHREADS / CC;     // rows per pass
+  const int cc = tid % CC, r0 = tid / CC;
+  const int col = cc * 8;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[bias_col(col + e)] : 0.0f;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int row = r0; row < TR; row += RS) {
+    T* p = dst(row, col);
+    if (p == nullptr) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(tile + row * (TC + 4) + col);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(tile + row * (TC + 4) + col + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (stats) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += v[e];
+        s2[e] += v[e] * v[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bv[e];
+    if constexpr (sizeof(T) == 2) {
+      T o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = from_f<T>(v[e]);
+      uint4 u;
+      __builtin_memcpy(&u, o, 16);
+      *reinterpret_cast<uint4*>(p) = u;
+    } else {
+      *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+  if (stats) {
+    __syncthreads();  // everyone is done reading the tile: reuse it for the column reduction
+    float* red = tile;  // [RS][TC][2]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * TC + col + e) * 2 + 0] = s1[e];
+      red[(r0 * TC + col + e) * 2 + 1] = s2[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < TC; c += NTHREADS) {
+      float a = 0.0f, b = 0.0f;
+      for (int r = 0; r < RS; ++r) {
+        a += red[(r * TC + c) * 2 + 0];
+        b += red[(r * TC + c) * 2 + 1];
+      }
+      stats[c] = a;
+      stats[ld_stats + c] = b;
+    }
+  }
+}
+
+// host: validate a C-ABI gather descriptor and convert it (gemm.hip)
+int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems);
+
+// 3x3 conv with the input tile + halo staged once per channel chunk (conv3x3.hip). Returns
+// false when the operand is not eligible (caller falls back to the generic gather GEMM).
+bool conv3x3_halo_eligible(const GatherArg& g, int N, int dtype);
+int64_t conv3x3_halo_tiles(const GatherArg& g);
+int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
+                        hipStream_t st);
+bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
+int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, hipStream_t st);
+bool halo_enabled();
+
+}  // namespace selunet

@@ -238,25 +238,80 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int64_t 
   coef[2 * C + c] = (float)k2;
 }
 
+// dy = k0*dA - k1 - k2*xhat = k0*dA - (k1 - k2*mean*invstd) - (k2*invstd)*y. Each thread owns a fixed
+// group of 8 channels (coefficients in registers) and strides over pixels: 16-B bf16 / 32-B fp32
+// vectors, one pass over dz and y, one write of dy.
 template <typename T>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                     const float* __restrict__ mean, const float* __restrict__ invstd,
                                     const float* __restrict__ coef, T* __restrict__ dy) {
-  const int64_t nv = m * C / 4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)((i * 4) % C);
-    const f32x4 yv = Vec4<T>::load(y + i * 4);
-    const f32x4 g = Vec4<T>::load(dz + i * 4);
-    f32x4 o;
+  const int CG = C >> 3;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
+  const int PL = TPB / CG;
+  const int c = cg * 8;
+  float sc[8], sh[8], k0[8], a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c + e];
+    sh[e] = shift[c + e];
+    k0[e] = coef[c + e];
+    const float k2i = coef[2 * C + c + e] * invstd[c + e];
+    a[e] = k2i;
+    b[e] = coef[C + c + e] - k2i * mean[c + e];
+  }
+  for (int64_t p = blockIdx.x * (int64_t)PL + pl; p < m; p += (int64_t)gridDim.x * PL) {
+    const int64_t off = p * C + c;
+    const f32x4 y0 = Vec4<T>::load(y + off), y1 = Vec4<T>::load(y + off + 4);
+    const f32x4 g0 = Vec4<T>::load(dz + off), g1 = Vec4<T>::load(dz + off + 4);
+    f32x4 o0, o1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float z = yv[e] * scale[c + e] + shift[c + e];
-      const float da = z > 0.0f ? g[e] : 0.0f;
-      const float xh = (yv[e] - mean[c + e]) * invstd[c + e];
-      o[e] = coef[c + e] * da - coef[C + c + e] - coef[2 * C + c + e] * xh;
+      o0[e] = (y0[e] * sc[e] + sh[e] > 0.0f ? k0[e] * g0[e] : 0.0f) - b[e] - a[e] * y0[e];
+      o1[e] = (y1[e] * sc[e + 4] + sh[e + 4] > 0.0f ? k0[e + 4] * g1[e] : 0.0f) - b[e + 4] - a[e + 4] * y1[e];
     }
-    Vec4<T>::store(dy + i * 4, o);
+    Vec4<T>::store(dy + off, o0);
+    Vec4<T>::store(dy + off + 4, o1);
+  }
+}
+
+// =========================================================================== first-layer im2col
+// x NCHW fp32 [n][c][h][w] -> out [n*h*w][k_pad] (dtype), column tap*c + ci of a 3x3 pad-1 window,
+// zero beyond 9c. Lets the C_in = 3 layer (model.py:29) run as a dense GEMM (forward and weight
+// gradient) instead of an element-wise gather.
+template <typename T>
+__global__ void im2col3x3_kernel(const float* __restrict__ x, int n, int c, int h, int w, int k_pad,
+                                 T* __restrict__ out) {
+  const int64_t M = (int64_t)n * h * w;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < M; p += (int64_t)gridDim.x * blockDim.x) {
+    const int xx = (int)(p % w);
+    const int64_t t = p / w;
+    const int yy = (int)(t % h);
+    const int64_t img = t / h;
+    T* row = out + p * k_pad;
+    for (int k0 = 0; k0 < k_pad; k0 += 8) {
+      T v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = k0 + e;
+        float f = 0.0f;
+        if (k < 9 * c) {
+          const int tap = k / c, ci = k - tap * c;
+          const int ys = yy + tap / 3 - 1, xs = xx + tap % 3 - 1;
+          if ((unsigned)ys < (unsigned)h && (unsigned)xs < (unsigned)w)
+            f = x[((img * c + ci) * h + ys) * (int64_t)w + xs];
+        }
+        v[e] = from_f<T>(f);
+      }
+      if constexpr (sizeof(T) == 2) {
+        uint4 o;
+        __builtin_memcpy(&o, v, 16);
+        *reinterpret_cast<uint4*>(row + k0) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(row + k0) = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        *reinterpret_cast<f32x4*>(row + k0 + 4) = f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+      }
+    }
   }
 }
 
@@ -665,10 +720,22 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
                          void* stream) {
   SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
                   "bn_bwd_apply: bad arguments");
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(m * c / 4, 8192)), dim3(TPB), 0,
+  SELUNET_REQUIRE(ok_channels(c), "bn_bwd_apply: C must be 64, 128, 256 or 512 (got %d)", c);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), 4096));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(TPB), 0,
                                        as_stream(stream), (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd,
                                        coef, (T*)dy));
   return check_launch("bn_bwd_apply");
+}
+
+int selunet_im2col3x3(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, int32_t k_pad, void* out,
+                      int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(x && out && n > 0 && c > 0 && h > 0 && w > 0 && k_pad >= 9 * c && k_pad % 8 == 0,
+                  "im2col3x3: bad arguments");
+  const int64_t M = (int64_t)n * h * w;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(im2col3x3_kernel<T>, dim3(grid_for(M, 8192)), dim3(TPB), 0, as_stream(stream),
+                                       x, n, c, h, w, k_pad, (T*)out));
+  return check_launch("im2col3x3");
 }
 
 int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,

@@ -97,17 +97,17 @@ class Engine:
         return packs
 
     # ------------------------------------------------------------------ forward pieces
-    def _cbr(self, ctx, name, P, B, n, h, w, *srcs):
+    def _cbr(self, ctx, name, P, B, n, h, w, *srcs, taps=9):
         fwd, _, kpad = ctx.wpack[name]
         co = fwd.shape[0]
         M = n * h * w
         dev = fwd.device
         y = torch.empty(M, co, dtype=self.dt, device=dev)
         stats = None
-        rows = (M + K.GEMM_BM - 1) // K.GEMM_BM
+        g = K.gather(n, h, w, taps, *srcs)
+        rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
         if ctx.training:
             stats = torch.empty(rows, 2, co, dtype=torch.float32, device=dev)
-        g = K.gather(n, h, w, 9, *srcs)
         ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
         K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
         mean, invstd, scale, shift = (torch.empty(co, dtype=torch.float32, device=dev) for _ in range(4))
@@ -150,7 +150,11 @@ class Engine:
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
         h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
-        e11 = c("encoder_layer_1_1", h1, w1, K.source(x, cin, layout=1))
+        # first layer (C_in = 3): explicit im2col, then a dense GEMM (taps = 1)
+        kpad0 = ctx.wpack["encoder_layer_1_1"][2]
+        ctx.cols = torch.empty(n * H * W, kpad0, dtype=self.dt, device=x.device)
+        K.call("selunet_im2col3x3", K.ptr(x), n, cin, H, W, kpad0, K.ptr(ctx.cols), self.code, self.stream)
+        e11 = self._cbr(ctx, "encoder_layer_1_1", P, B, n, h1, w1, K.source(ctx.cols, kpad0), taps=1)
         e12 = c("encoder_layer_1_2", h1, w1, e11.src())
         p1 = self._pool(ctx, "pool1", e12)
         e21 = c("encoder_layer_2_1", h2, w2, K.source(p1, 64))
@@ -182,7 +186,7 @@ class Engine:
         return tuple(outs), ctx
 
     # ------------------------------------------------------------------ backward pieces
-    def _cbr_bwd(self, ctx, name, dz, G, input_srcs, dgrad_split=None, need_dgrad=True):
+    def _cbr_bwd(self, ctx, name, dz, G, input_srcs, dgrad_split=None, need_dgrad=True, q_taps=9, ci_real=None):
         """BN+ReLU backward then conv weight/bias grads; returns the data gradient (or split pair)."""
         st: BNState = ctx.bn[name]
         M, co, dev = st.n * st.h * st.w, st.c, st.y.device
@@ -202,12 +206,13 @@ class Engine:
                K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
         ci = sum(s.channels for s in input_srcs)
-        ld = K.query("selunet_wgrad_ld", 9 * ci)
+        ld = K.query("selunet_wgrad_ld", q_taps * ci)
         packed = torch.zeros(co, ld, dtype=torch.float32, device=dev)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
-        gq = K.gather(st.n, st.h, st.w, 9, *input_srcs)
+        gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
         K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
-        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
+        ci_w = ci if ci_real is None else ci_real  # im2col operand: packed columns are (tap, ci) already
+        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci_w, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
         if not need_dgrad:
             return None
         _, wd, _ = ctx.wpack[name]
@@ -301,4 +306,4 @@ class Engine:
         dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64)])
         dz = self._pool_bwd(e12, dp1, dskip1)
         dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()])
-        cb("encoder_layer_1_1", dz, [K.source(ctx.x, cin, layout=1)], need_dgrad=False)
+        cb("encoder_layer_1_1", dz, [K.source(ctx.cols, ctx.cols.shape[1])], need_dgrad=False, q_taps=1, ci_real=cin)

@@ -140,7 +140,7 @@ def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outp
            "meta_steps": steps, "meta_chunks": chunks, "meta_seed": seed, "meta_data_seed": data_seed}
     out["x_sha1"] = np.bytes_(hashlib.sha1(x.tobytes()).hexdigest())
     out["label_sha1"] = np.bytes_(hashlib.sha1(lab.tobytes()).hexdigest())
-    if full_outputs:
+    if full_outputs and n * size * size <= 65536:  # inputs are regenerated from the seed for big batches
         out["x"] = x
         out["label"] = lab
     for s in range(steps):
@@ -331,5 +331,5 @@ if __name__ == "__main__":
     step_fixture("step_nosel_n2_64.npz", 2, 64, selective=False, steps=2)
     step_fixture("step_sel_lamb8_n3_32.npz", 3, 32, selective=True, lamb=8, steps=1)
     step_fixture("dp_sel_n8_32_c4.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=4)
-    step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=False)
+    step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=True)
     eval_fixture("eval_sel_n4_64.npz")

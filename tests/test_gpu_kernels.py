@@ -58,6 +58,9 @@ def pack(w, dt=torch.float32):
     (64, 64, 128, 2, 8, 8, True),      # two-source (torch.cat) gather
     (256, 256, 256, 1, 4, 4, True),
     (64, 0, 128, 3, 5, 7, True),       # M not a multiple of the 128-row tile
+    (64, 0, 64, 2, 32, 32, True),      # 16x16 halo-tile kernel
+    (64, 64, 128, 1, 16, 48, True),    # halo kernel, two sources, BN = 128
+    (128, 0, 256, 2, 20, 24, True),    # halo kernel, partial edge tiles
 ])
 def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform):
     x0 = gen(n, cin0, h, w, seed=1)
@@ -81,10 +84,11 @@ def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform):
         srcs.append(K.source(x1d, cin1, s1d, t1d))
     M = n * h * w
     y = torch.empty(M, cout, device=DEV)
-    rows = (M + 127) // 128
+    g = K.gather(n, h, w, 9, *srcs)
+    rows = K.query("selunet_gemm_stats_rows", g, cout, K.F32)
     stats = torch.empty(rows, 2, cout, device=DEV)
     ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
-    K.call("selunet_gemm_gather", K.gather(n, h, w, 9, *srcs), K.ptr(fwd), cout, kpad, ep, K.F32, K.stream_ptr())
+    K.call("selunet_gemm_gather", g, K.ptr(fwd), cout, kpad, ep, K.F32, K.stream_ptr())
     torch.cuda.synchronize()
     assert rel(nchw(y.cpu(), n, h, w), ref) < TOL
     st = stats.cpu().double().sum(0)
@@ -106,9 +110,11 @@ def test_conv3x3_fwd_small_c_nchw():
     assert rel(nchw(y.cpu(), n, h, w), ref) < TOL
 
 
-@pytest.mark.parametrize("cin,cout,split", [(64, 64, 0), (128, 64, 64), (512, 256, 256), (64, 128, 0)])
-def test_conv3x3_dgrad(cin, cout, split):
-    n, h, w = 2, 8, 8
+@pytest.mark.parametrize("cin,cout,split,h,w", [(64, 64, 0, 8, 8), (128, 64, 64, 8, 8), (512, 256, 256, 8, 8),
+                                                (64, 128, 0, 8, 8), (64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
+                                                (256, 128, 128, 16, 48)])
+def test_conv3x3_dgrad(cin, cout, split, h, w):
+    n = 2
     wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
     dy = gen(n, cout, h, w, seed=7)
     x = gen(n, cin, h, w, seed=8).requires_grad_()
@@ -301,11 +307,13 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
-@pytest.mark.parametrize("cin0,cin1,cout,small", [(64, 0, 64, False), (64, 64, 128, False), (256, 0, 512, False),
-                                                  (3, 0, 64, True)])
-def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small):
-    """bf16 operands, fp32 accumulation: compared with fp32 torch on the same bf16-rounded data."""
-    n, h, w = 2, 16, 16
+@pytest.mark.parametrize("cin0,cin1,cout,small,h,w", [(64, 0, 64, False, 16, 16), (64, 64, 128, False, 16, 16),
+                                                      (256, 0, 512, False, 16, 16), (3, 0, 64, True, 16, 16),
+                                                      (128, 0, 64, False, 20, 40), (64, 128, 64, False, 24, 17)])
+def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small, h, w):
+    """bf16 operands, fp32 accumulation: compared with fp32 torch on the same bf16-rounded data
+    (sizes >= 16 take the halo-tiled kernels, incl. partial edge tiles)."""
+    n = 2
     x0 = _bf(gen(n, cin0, h, w, seed=40))
     x1 = _bf(gen(n, cin1, h, w, seed=41)) if cin1 else None
     s0, t0 = bn_fold(cin0, 42)
