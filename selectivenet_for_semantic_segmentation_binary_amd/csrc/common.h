@@ -52,17 +52,17 @@ template <> struct Vec4<__bf16> {
 template <typename T> __device__ inline float to_f(T v) { return (float)v; }
 template <typename T> __device__ inline T from_f(float v) { return (T)v; }
 
-__device__ inline float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 // numerically stable softplus(x) = log(1 + exp(x))
-__device__ inline float softplusf_(float x) { return fmaxf(x, 0.0f) + log1pf(__expf(-fabsf(x))); }
+__device__ __forceinline__ float softplusf_(float x) { return fmaxf(x, 0.0f) + log1pf(__expf(-fabsf(x))); }
 
 // wave64 sum
-__device__ inline float wave_sum(float v) {
+__device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ inline double wave_sum(double v) {
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;

@@ -44,8 +44,9 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int half = lane >> 5, l32 = lane & 31;
 
-  const int n_tile = blockIdx.x % n_tiles;
-  const int ptile = blockIdx.x / n_tiles;
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n_tile = lb % n_tiles;
+  const int ptile = lb / n_tiles;
   const int tx_t = ptile % tiles_x;
   const int rest = ptile / tiles_x;
   const int ty_t = rest % tiles_y;
@@ -77,7 +78,7 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     a_s = s;
     a_c = c + cc * E;
     if ((unsigned)ys < (unsigned)g.h && (unsigned)xs < (unsigned)g.w) {
-      const SrcArg& sa = g.src[s];
+      const SrcArg sa = pick_src(g, s);
       ra = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
                                           (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + a_c);
       aok = true;
@@ -87,7 +88,7 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     const int hidx = round * HTHREADS + tid;
     if (hidx >= HPIX * 8) return;
     const int hp = hidx >> 3, cc = hidx & 7;
-    const SrcArg& sa = g.src[a_s];
+    const SrcArg sa = pick_src(g, a_s);
     uint4 v = ra;
     if (sa.scale) v = aok ? transform16<T>(v, sa.scale, sa.shift, a_c, sa.relu) : make_uint4(0, 0, 0, 0);
     *reinterpret_cast<uint4*>(As + (buf * HPIX + hp) * ROWB + cc * 16) = v;
@@ -223,8 +224,9 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
   const int half = lane >> 5, l32 = lane & 31;
   const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
-  const int cot = blockIdx.x % co_tiles;
-  const int rest = blockIdx.x / co_tiles;
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int cot = lb % co_tiles;
+  const int rest = lb / co_tiles;
   const int cik = rest % ci_chunks;
   const int64_t split = rest / ci_chunks;
   const int i0 = cot * BI;
@@ -239,7 +241,7 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
     xc -= Q.src[0].C;
     xs_src = 1;
   }
-  const SrcArg& xa = Q.src[xs_src];
+  const SrcArg xa = pick_src(Q, xs_src);
   const SrcArg& pa = P.src[0];
   const int H = P.h, W = P.w;
 

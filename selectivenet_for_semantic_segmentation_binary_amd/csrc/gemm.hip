@@ -23,7 +23,7 @@
 
 namespace selunet {
 
-template <typename T, int BN>
+template <typename T, int BN, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
 gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles) {
   constexpr int E = 16 / sizeof(T);          // elements per 16-B vector
@@ -45,8 +45,9 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   const int wm = wave >> 1, wn = wave & 1;
   const int half = lane >> 5, l32 = lane & 31;
 
-  const int n_tile = blockIdx.x % n_tiles;
-  const int64_t m_tile = blockIdx.x / n_tiles;
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n_tile = lb % n_tiles;
+  const int64_t m_tile = lb / n_tiles;
   const int64_t m0 = m_tile * BM;
   const int n0 = n_tile * BN;
 
@@ -72,9 +73,9 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   uint4 rb[BR];
   int st_src = 0, st_c = 0;  // transform selector of the staged slice
 
-  auto load_stage = [&](int kc) {
+  auto load_stage = [&](int kc) __attribute__((always_inline)) {
     const int k0 = kc * BKE;
-    if (!g.small) {
+    if constexpr (!SMALL) {
       const int tap = k0 / g.Ctot;
       int c0 = k0 - tap * g.Ctot;
       int s = 0;
@@ -84,7 +85,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       }
       st_src = s;
       st_c = c0 + cc * E;
-      const SrcArg& sa = g.src[s];
+      const SrcArg sa = pick_src(g, s);
       const T* base = reinterpret_cast<const T*>(sa.data);
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
@@ -116,16 +117,36 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     }
   };
 
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf) __attribute__((always_inline)) {
     unsigned char* a_dst = As + buf * BM * ROWB;
     unsigned char* b_dst = Bs + buf * BN * ROWB;
-    const SrcArg& sa = g.src[st_src];
-    const bool xf = !g.small && sa.scale != nullptr;
+    const SrcArg sa = pick_src(g, st_src);
+    if (!SMALL && sa.scale != nullptr) {
+      // folded BN + ReLU of the producer; the 8 (bf16) / 4 (fp32) channel coefficients are the
+      // same for every row this thread stages
+      float scv[E], shv[E];
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      uint4 v = ra[i];
-      if (xf) v = rok[i] ? transform16<T>(v, sa.scale, sa.shift, st_c, sa.relu) : make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = v;
+      for (int e = 0; e < E; ++e) {
+        scv[e] = sa.scale[st_c + e];
+        shv[e] = sa.shift[st_c + e];
+      }
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        T v[E];
+        __builtin_memcpy(v, &ra[i], 16);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          float f = to_f(v[e]) * scv[e] + shv[e];
+          f = sa.relu ? fmaxf(f, 0.0f) : f;
+          v[e] = from_f<T>(rok[i] ? f : 0.0f);
+        }
+        uint4 o;
+        __builtin_memcpy(&o, v, 16);
+        *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = o;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
@@ -198,21 +219,17 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 // [32 rows (m)][BI or BJ] fp32 so the MFMA operands (one element per lane: A[i][k], B[k][j])
 // are single conflict-free ds_read_b32 along a row.
 template <typename T>
-__device__ inline f32x4 gather_vec4(const GatherArg& g, int64_t m, int k, int tap, int s, int c,
+__device__ __forceinline__ f32x4 gather_vec4(const GatherArg& g, int64_t m, int k, int tap, int s, int c,
                                     bool vec) {
   if (!vec) {
     return f32x4{gather_scalar<T>(g, m, k), gather_scalar<T>(g, m, k + 1), gather_scalar<T>(g, m, k + 2),
                  gather_scalar<T>(g, m, k + 3)};
   }
   if (m >= g.M) return f32x4{0, 0, 0, 0};
-  const int x = (int)(m % g.w);
-  const int64_t t = m / g.w;
-  const int y = (int)(t % g.h);
-  const int img = (int)(t / g.h);
-  int ys, xs;
-  if (!src_pixel(g, tap, y, x, ys, xs)) return f32x4{0, 0, 0, 0};
-  const SrcArg& sa = g.src[s];
-  f32x4 v = Vec4<T>::load(reinterpret_cast<const T*>(sa.data) + (((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c);
+  const int64_t pix = src_index(g, m, tap);
+  if (pix < 0) return f32x4{0, 0, 0, 0};
+  const SrcArg sa = pick_src(g, s);
+  f32x4 v = Vec4<T>::load(reinterpret_cast<const T*>(sa.data) + pix * sa.C + c);
   if (sa.scale) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -223,7 +240,7 @@ __device__ inline f32x4 gather_vec4(const GatherArg& g, int64_t m, int k, int ta
   return v;
 }
 
-template <typename T, int BI, int BJ>
+template <typename T, int BI, int BJ, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
 gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk,
                   int tiles_j, int tiles) {
@@ -242,8 +259,9 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
   const int wi = wave >> 1, wj = wave & 1;
   const int half = lane >> 5, l32 = lane & 31;
 
-  const int tile = blockIdx.x % tiles;
-  const int64_t split = blockIdx.x / tiles;
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lb % tiles;
+  const int64_t split = lb / tiles;
   const int i0 = (tile / tiles_j) * BI;
   const int j0 = (tile % tiles_j) * BJ;
   const int64_t mb = split * mchunk;
@@ -255,7 +273,7 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
   const int qc = tid % CPJ, qr = tid / CPJ;
   const int pk = i0 + pc * 4, qk = j0 + qc * 4;
   int ptap = 0, ps = 0, pch = 0, qtap = 0, qs = 0, qch = 0;
-  const bool pvec = !P.small, qvec = !Q.small;
+  const bool pvec = !SMALL || !P.small, qvec = !SMALL || !Q.small;
   if (pvec) {
     ptap = pk / P.Ctot;
     pch = pk - ptap * P.Ctot;
@@ -281,7 +299,7 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
       rq[i] = (qin && m < me) ? gather_vec4<T>(Q, m, qk, qtap, qs, qch, qvec) : f32x4{0, 0, 0, 0};
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PI; ++i) *reinterpret_cast<f32x4*>(&Ps[buf][pr + RPI * i][pc * 4]) = rp[i];
 #pragma unroll
@@ -340,7 +358,7 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
 // the k-run m = 8*half .. 8*half+7 of its column. Rows are padded by 64 B so the 32 lanes of a
 // read touch 64 distinct banks (row stride = 16 dwords mod 64).
 
-__device__ inline uint4 gather_vec8_bf16(const GatherArg& g, int64_t m, int k, int tap, int s, int c, bool vec,
+__device__ __forceinline__ uint4 gather_vec8_bf16(const GatherArg& g, int64_t m, int k, int tap, int s, int c, bool vec,
                                          bool in) {
   if (!in || m >= g.M) return make_uint4(0, 0, 0, 0);
   if (!vec) {
@@ -351,20 +369,15 @@ __device__ inline uint4 gather_vec8_bf16(const GatherArg& g, int64_t m, int k, i
     __builtin_memcpy(&o, v, 16);
     return o;
   }
-  const int x = (int)(m % g.w);
-  const int64_t t = m / g.w;
-  const int y = (int)(t % g.h);
-  const int img = (int)(t / g.h);
-  int ys, xs;
-  if (!src_pixel(g, tap, y, x, ys, xs)) return make_uint4(0, 0, 0, 0);
-  const SrcArg& sa = g.src[s];
-  uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(sa.data) +
-                                              (((int64_t)img * g.hs + ys) * g.ws + xs) * sa.C + c);
+  const int64_t pix = src_index(g, m, tap);
+  if (pix < 0) return make_uint4(0, 0, 0, 0);
+  const SrcArg sa = pick_src(g, s);
+  uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(sa.data) + pix * sa.C + c);
   if (sa.scale) raw = transform16<__bf16>(raw, sa.scale, sa.shift, c, sa.relu);
   return raw;
 }
 
-template <int BI, int BJ>
+template <int BI, int BJ, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
 gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk, int tiles_j,
                        int tiles) {
@@ -386,8 +399,9 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
   const int half = lane >> 5, l32 = lane & 31;
   const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
-  const int tile = blockIdx.x % tiles;
-  const int64_t split = blockIdx.x / tiles;
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lb % tiles;
+  const int64_t split = lb / tiles;
   const int i0 = (tile / tiles_j) * BI;
   const int j0 = (tile % tiles_j) * BJ;
   const int64_t mb = split * mchunk;
@@ -398,7 +412,7 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
   const int qc = tid % CPJ, qr = tid / CPJ;
   const int pk = i0 + pc * 8, qk = j0 + qc * 8;
   int ptap = 0, ps = 0, pch = 0, qtap = 0, qs = 0, qch = 0;
-  const bool pvec = !P.small, qvec = !Q.small;
+  const bool pvec = !SMALL || !P.small, qvec = !SMALL || !Q.small;
   if (pvec) {
     ptap = pk / P.Ctot;
     pch = pk - ptap * P.Ctot;
@@ -424,7 +438,7 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
       rq[i] = gather_vec8_bf16(Q, m < me ? m : Q.M, qk, qtap, qs, qch, qvec, qin);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PI; ++i) *reinterpret_cast<uint4*>(&Ps[buf][pr + RPI * i][pc * 8]) = rp[i];
 #pragma unroll
@@ -503,6 +517,8 @@ int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems)
   g.hs = a->taps == 4 ? 2 * a->h : a->h;
   g.ws = a->taps == 4 ? 2 * a->w : a->w;
   g.M = (int64_t)a->n * a->h * a->w;
+  SELUNET_REQUIRE(g.M * (a->taps == 4 ? 4 : 1) < (int64_t(1) << 31), "gather grid too large (%lld rows)",
+                  (long long)g.M);
   int ctot = 0;
   bool vec = true;
   for (int s = 0; s < a->nsrc; ++s) {
@@ -532,17 +548,39 @@ int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems)
   return 0;
 }
 
+template <typename T, int BN, bool SMALL>
+static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st);
+template <typename T, int BI, int BJ, bool SMALL>
+static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
+                              hipStream_t st);
+
 template <typename T, int BN>
 static void launch_gather(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
+  if (g.small) {
+    launch_gather_impl<T, BN, true>(g, b, N, k_pad, ep, st);
+    return;
+  }
+  launch_gather_impl<T, BN, false>(g, b, N, k_pad, ep, st);
+}
+
+template <typename T, int BN, bool SMALL>
+static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
   const int n_tiles = N / BN;
   const int64_t m_tiles = cdiv(g.M, BM);
-  hipLaunchKernelGGL((gemm_gather_kernel<T, BN>), dim3((unsigned)(m_tiles * n_tiles)), dim3(256), 0, st, g,
+  hipLaunchKernelGGL((gemm_gather_kernel<T, BN, SMALL>), dim3((unsigned)(m_tiles * n_tiles)), dim3(256), 0, st, g,
                      reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles);
 }
 
 template <typename T, int BI, int BJ>
 static void launch_wgrad(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
                          hipStream_t st) {
+  if (p.small || q.small) launch_wgrad_impl<T, BI, BJ, true>(p, q, out, ldo, ni, nj_pad, st);
+  else launch_wgrad_impl<T, BI, BJ, false>(p, q, out, ldo, ni, nj_pad, st);
+}
+
+template <typename T, int BI, int BJ, bool SMALL>
+static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
+                              hipStream_t st) {
   const int tiles_j = nj_pad / BJ;
   const int tiles = (ni / BI) * tiles_j;
   const int64_t M = p.M;
@@ -550,10 +588,10 @@ static void launch_wgrad(const GatherArg& p, const GatherArg& q, float* out, int
   int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
   splits = cdiv(M, mchunk);
   if constexpr (std::is_same<T, float>::value)
-    hipLaunchKernelGGL((gemm_wgrad_kernel<T, BI, BJ>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q, out,
+    hipLaunchKernelGGL((gemm_wgrad_kernel<T, BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q, out,
                        ldo, mchunk, tiles_j, tiles);
   else
-    hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<BI, BJ>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q,
+    hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q,
                        out, ldo, mchunk, tiles_j, tiles);
 }
 

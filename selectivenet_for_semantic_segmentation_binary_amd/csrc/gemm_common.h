@@ -27,11 +27,26 @@ struct GatherArg {
   SrcArg src[2];
 };
 
+// Select a source by a runtime index without indexing the kernel-argument array (a dynamic
+// index forces the whole argument struct onto the scratch stack: ~200 B of scratch writes per
+// thread, visible as WRITE_SIZE far above the output size).
+__device__ __forceinline__ SrcArg pick_src(const GatherArg& g, int s) {
+  SrcArg r;
+  r.data = s ? g.src[1].data : g.src[0].data;
+  r.scale = s ? g.src[1].scale : g.src[0].scale;
+  r.shift = s ? g.src[1].shift : g.src[0].shift;
+  r.C = s ? g.src[1].C : g.src[0].C;
+  r.relu = s ? g.src[1].relu : g.src[0].relu;
+  r.layout = s ? g.src[1].layout : g.src[0].layout;
+  r.pad = 0;
+  return r;
+}
+
 constexpr int BM = SELUNET_GEMM_BM;
 constexpr int ROWB = 144;  // padded LDS row bytes for a 128-B K slice
 
 // --------------------------------------------------------------------------- gather helpers
-__device__ inline void tap_offset(int taps, int tap, int& dy, int& dx) {
+__device__ __forceinline__ void tap_offset(int taps, int tap, int& dy, int& dx) {
   if (taps == 9) {
     dy = tap / 3 - 1;
     dx = tap - (tap / 3) * 3 - 1;
@@ -45,7 +60,7 @@ __device__ inline void tap_offset(int taps, int tap, int& dy, int& dx) {
 }
 
 // source pixel of row pixel (y, x) for `tap`; returns false when it falls into the zero pad.
-__device__ inline bool src_pixel(const GatherArg& g, int tap, int y, int x, int& ys, int& xs) {
+__device__ __forceinline__ bool src_pixel(const GatherArg& g, int tap, int y, int x, int& ys, int& xs) {
   int dy, dx;
   tap_offset(g.taps, tap, dy, dx);
   if (g.taps == 4) {
@@ -58,9 +73,22 @@ __device__ inline bool src_pixel(const GatherArg& g, int tap, int y, int x, int&
   return (unsigned)ys < (unsigned)g.hs && (unsigned)xs < (unsigned)g.ws;
 }
 
+// Linear index (in the source grid) of the pixel that row m reads for `tap`, or -1 inside the
+// zero pad. Pointwise operands need no decode; otherwise 32-bit division (M < 2^31 is checked
+// on the host).
+__device__ __forceinline__ int64_t src_index(const GatherArg& g, int64_t m, int tap) {
+  if (g.taps == 1) return m;
+  const unsigned mu = (unsigned)m;
+  const unsigned x = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
+  const unsigned y = t % (unsigned)g.h, img = t / (unsigned)g.h;
+  int ys, xs;
+  if (!src_pixel(g, tap, (int)y, (int)x, ys, xs)) return -1;
+  return ((int64_t)img * g.hs + ys) * g.ws + xs;
+}
+
 // One gathered element (slow path, small C / non-vector channel counts). Applies the transform.
 template <typename T>
-__device__ inline float gather_scalar(const GatherArg& g, int64_t m, int k) {
+__device__ __forceinline__ float gather_scalar(const GatherArg& g, int64_t m, int k) {
   if (m >= g.M || k >= g.K) return 0.0f;
   const int tap = k / g.Ctot;
   int c = k - tap * g.Ctot;
@@ -75,7 +103,7 @@ __device__ inline float gather_scalar(const GatherArg& g, int64_t m, int k) {
   const int img = (int)(t / g.h);
   int ys, xs;
   if (!src_pixel(g, tap, y, x, ys, xs)) return 0.0f;
-  const SrcArg& sa = g.src[s];
+  const SrcArg sa = pick_src(g, s);
   float v;
   if (sa.layout == 1) {
     v = reinterpret_cast<const float*>(sa.data)[(((int64_t)img * sa.C + c) * g.hs + ys) * g.ws + xs];
@@ -109,7 +137,7 @@ template <> struct Mma<__bf16> {
 
 // apply folded BN + ReLU to a 16-B vector of T (E elements), channel base c
 template <typename T>
-__device__ inline uint4 transform16(uint4 raw, const float* scale, const float* shift, int c, int relu) {
+__device__ __forceinline__ uint4 transform16(uint4 raw, const float* scale, const float* shift, int c, int relu) {
   constexpr int E = 16 / sizeof(T);
   T v[E];
   __builtin_memcpy(v, &raw, 16);
@@ -136,12 +164,21 @@ struct EpiArg {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// Bijective remap of blockIdx.x so that consecutive logical blocks (which share operand tiles)
+// run on the same XCD: the dispatcher deals blocks round-robin over the 8 XCDs, each with its own
+// L2. Speed only, never correctness (MI355X guide T1, bijective form for nb % 8 != 0).
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
+  const unsigned xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+  const unsigned base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
 // --------------------------------------------------------------------------- LDS-staged epilogue
 // Accumulators of the wave's MT x NT 32x32 subtiles (tile coords (wr0 + a*32, wc0 + b*32)) ->
 // fp32 LDS tile [TR][TC + 4]. C/D layout of the 32x32 MFMAs: col = lane & 31,
 // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
 template <int MT, int NT, int TC>
-__device__ inline void acc_to_lds(float* tile, const f32x16 (&acc)[MT][NT], int wr0, int wc0, int lane) {
+__device__ __forceinline__ void acc_to_lds(float* tile, const f32x16 (&acc)[MT][NT], int wr0, int wc0, int lane) {
   const int half = lane >> 5, l32 = lane & 31;
 #pragma unroll
   for (int a = 0; a < MT; ++a)
@@ -158,7 +195,7 @@ __device__ inline void acc_to_lds(float* tile, const f32x16 (&acc)[MT][NT], int 
 // squares over the stored rows (before the bias) go to stats[0][col], stats[1][col] of the
 // block's slab row (stride ld_stats between the two).
 template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
-__device__ inline void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
+__device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
                                       float* stats, int ld_stats) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass

@@ -111,7 +111,7 @@ def run_fixture(fname, strict_steps=1):
         pv = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
         # Adam moves an element by ~lr*sign(g); elements whose gradient sits at rounding level
         # (pre-BN biases, near-tie ReLU/max-pool routes) can move the other way: floor 2.5*lr.
-        fails += G.check_tensors(d, pre + "param", pv, rtol=1e-5, atol=2.5e-3)
+        fails += G.check_tensors(d, pre + "param", pv, rtol=1e-5, atol=2.5e-3 if strict else 5e-3)
         bufs = dict(net.named_buffers())
         for k, v in bufs.items():
             if "running" in k:
