@@ -57,44 +57,66 @@ def parse():
 
 
 class KernelTimer:
-    """Brackets selected C-ABI entry points with HIP events on the launch stream and counts
-    their algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM)."""
+    """Brackets the MFMA GEMM entry points with HIP events on the launch stream (torch's current
+    stream, the one the kernels are launched on) and attributes each launch to the kernel it
+    dispatches to (selunet_gemm_kernel_name), with its algorithmic FLOPs (2*M*N*K of the true,
+    unpadded GEMM) and algorithmic HBM bytes (each operand tensor read once, output written once)."""
 
-    NAMES = ("selunet_gemm_gather", "selunet_gemm_wgrad")
+    ENTRY = ("selunet_gemm_gather", "selunet_gemm_wgrad")
 
-    def __init__(self):
+    def __init__(self, esz):
         self.active = False
-        self.events = {n: [] for n in self.NAMES}
-        self.flops = {n: 0.0 for n in self.NAMES}
-        self.launches = {n: 0 for n in self.NAMES}
+        self.esz = esz
+        self.rec = {}  # kernel name -> list of (start, end, flops, bytes)
 
     @staticmethod
     def _k(g):
         return g.taps * sum(g.src[i].channels for i in range(g.nsrc))
 
+    def _src_bytes(self, g):
+        hs, ws = (2 * g.h, 2 * g.w) if g.taps == 4 else (g.h, g.w)
+        return sum(g.n * hs * ws * g.src[i].channels * (4 if g.src[i].layout == 1 else self.esz)
+                   for i in range(g.nsrc))
+
     def __call__(self, name, args, fn):
-        if not self.active or name not in self.events:
+        if not self.active or name not in self.ENTRY:
             return fn()
+        if name == "selunet_gemm_gather":
+            g, n_cols, mode = args[0], args[2], args[4].mode
+            kname = K.query("selunet_gemm_kernel_name", g, None, n_cols, mode, args[5]).decode()
+            m = g.n * g.h * g.w
+            flops = 2.0 * m * n_cols * self._k(g)
+            nbytes = self._src_bytes(g) + m * n_cols * self.esz + n_cols * self._k(g) * self.esz
+        else:
+            gp, gq = args[0], args[1]
+            kname = K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, args[3]).decode()
+            flops = 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
+            nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         rc = fn()
         e.record()
-        self.events[name].append((s, e))
-        if name == "selunet_gemm_gather":
-            g, n_cols = args[0], args[2]
-            self.flops[name] += 2.0 * g.n * g.h * g.w * n_cols * self._k(g)
-        else:
-            gp, gq = args[0], args[1]
-            self.flops[name] += 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
-        self.launches[name] += 1
+        self.rec.setdefault(kname, []).append((s, e, flops, nbytes))
         return rc
 
     def summary(self):
         out = {}
-        for n in self.NAMES:
-            ms = sum(s.elapsed_time(e) for s, e in self.events[n])
-            out[n] = {"ms": ms, "launches": self.launches[n], "flops": self.flops[n]}
+        for k, lst in self.rec.items():
+            out[k] = {"ms": sum(s.elapsed_time(e) for s, e, _, _ in lst), "launches": len(lst),
+                      "flops": sum(f for _, _, f, _ in lst), "bytes": sum(b for _, _, _, b in lst)}
         return out
+
+
+def load_traffic(kernel):
+    """PMC-measured HBM bytes per launch for `kernel` from the committed profile summary
+    (profiles/*_traffic.json, written by tools/pmc_summary.py --traffic), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if kernel in d.get("kernels", {}):
+            return d["kernels"][kernel], os.path.relpath(path, REPO)
+    return None, None
 
 
 def cpu_baseline(args):
@@ -147,7 +169,7 @@ def main():
     lt = torch.tensor(lab[lo:hi], device=dev)
     del x, lab
 
-    timer = KernelTimer()
+    timer = KernelTimer(2 if dt == torch.bfloat16 else 4)
     if not args.no_kernel_timing:
         K.set_call_hook(timer)
 
@@ -192,13 +214,20 @@ def main():
         d = ksum[dom]
         peak, unit = PEAK[args.dtype]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12 if d["ms"] > 0 else 0.0
+        launches = max(1, d["launches"])
+        traffic, tsrc = load_traffic(dom)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 4), "traffic": None,
-                "per_launch_ms": round(d["ms"] / max(1, d["launches"]), 4),
+                "frac": round(achieved / peak, 4),
+                "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                "traffic_source": tsrc,
+                "algorithmic_flops_per_launch": d["flops"] / launches,
+                "algorithmic_bytes_per_launch": d["bytes"] / launches,
+                "per_launch_ms": round(d["ms"] / launches, 4),
                 "launches": d["launches"], "kernel_share_of_step": round(d["ms"] / (elapsed * 1e3), 4),
-                "all": {n: {"ms_per_step": round(v["ms"] / args.steps, 3),
-                            "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] else 0.0}
-                        for n, v in ksum.items()}}
+                "all": {n: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] // args.steps,
+                            "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] else 0.0,
+                            "hbm_gbs_algorithmic": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else 0.0}
+                        for n, v in sorted(ksum.items(), key=lambda kv: -kv[1]["ms"])}}
         if args.layer_report and rank == 0:
             print(json.dumps(roof, indent=1), file=sys.stderr)
     whole = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * value / 1e3  # TFLOP/s whole step

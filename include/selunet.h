@@ -110,6 +110,10 @@ int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, 
 /* Rows of the stats slab selunet_gemm_gather writes for this operand (pixel tiles of the
  * kernel it dispatches to: 16x16 halo tiles for 3x3 taps, else 128-row tiles); -1 on error. */
 int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t dtype);
+/* Name of the kernel a selunet_gemm_gather (q == NULL; mode = epilogue mode) or
+ * selunet_gemm_wgrad (q = the Q operand) call with these operands dispatches to. */
+const char* selunet_gemm_kernel_name(const selunet_gather* a, const selunet_gather* q, int32_t n_cols,
+                                     int32_t mode, int32_t dtype);
 /* out[ni][nj] += sum_m G_p[m][i] * G_q[m][j] (fp32 atomics; out zeroed by the caller).
  * Replaces the weight-gradient of conv2d / conv_transpose2d (train.py:208 backward). */
 int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out,

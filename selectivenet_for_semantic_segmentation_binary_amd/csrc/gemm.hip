@@ -615,6 +615,31 @@ extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_co
   return cdiv(g.M, BM);
 }
 
+// Name of the kernel selunet_gemm_gather / selunet_gemm_wgrad dispatch to for these operands
+// (profiling and roofline attribution; matches the rocprofv3 kernel names' template arguments).
+extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const selunet_gather* q, int32_t n_cols,
+                                                int32_t mode, int32_t dtype) {
+  const bool bf = dtype == SELUNET_BF16;
+  const int esz = bf ? 2 : 4;
+  GatherArg g;
+  if (q == nullptr) {
+    if (make_gather(a, dtype, g, 16 / esz)) return "invalid";
+    if (mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) {
+      // (SPLIT epilogues in this network split the columns in half: torch.cat of equal halves)
+      const bool bn128 = n_cols % 128 == 0 && !(mode == SELUNET_EP_SPLIT && (n_cols / 2) % 128 != 0);
+      return bf ? (bn128 ? "conv3x3_halo<bf16,128>" : "conv3x3_halo<bf16,64>")
+                : (bn128 ? "conv3x3_halo<f32,128>" : "conv3x3_halo<f32,64>");
+    }
+    return bf ? "gemm_gather<bf16>" : "gemm_gather<f32>";
+  }
+  GatherArg gq;
+  const int vec = bf ? 8 : 4;
+  if (make_gather(a, dtype, g, vec) || make_gather(q, dtype, gq, vec)) return "invalid";
+  if (halo_enabled() && conv3x3_wgrad_halo_eligible(g, gq, dtype))
+    return g.K % 128 == 0 ? "conv3x3_wgrad_halo<128>" : "conv3x3_wgrad_halo<64>";
+  return bf ? "gemm_wgrad_bf16" : "gemm_wgrad<f32>";
+}
+
 extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
                                    const selunet_epilogue* ep, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");

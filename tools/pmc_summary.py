@@ -1,7 +1,39 @@
-"""Aggregate rocprofv3 --pmc counter CSVs per kernel (test/profiling infrastructure)."""
+"""Aggregate rocprofv3 --pmc counter CSVs per kernel (profiling infrastructure).
+
+    python tools/pmc_summary.py gpurun_out/pmc1/p_counter_collection.csv [N]
+    python tools/pmc_summary.py --traffic profiles/r01_traffic.json FETCH.csv WRITE.csv
+
+--traffic writes, per kernel (named as bench.py / selunet_gemm_kernel_name name them), the HBM
+bytes per launch: FETCH_SIZE x 2 (on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
+coalesced streaming read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (exact for 16-B stores), both
+in KiB units as rocprofv3 reports them.
+"""
 import csv
+import json
+import re
 import sys
 from collections import defaultdict
+
+# rocprofv3 kernel-name pattern -> selunet kernel name
+NAME_MAP = [
+    (r"conv3x3_halo_kernelIDF16bLi128", "conv3x3_halo<bf16,128>"),
+    (r"conv3x3_halo_kernelIDF16bLi64", "conv3x3_halo<bf16,64>"),
+    (r"conv3x3_halo_kernelIfLi128", "conv3x3_halo<f32,128>"),
+    (r"conv3x3_halo_kernelIfLi64", "conv3x3_halo<f32,64>"),
+    (r"conv3x3_wgrad_halo_kernel<128>|conv3x3_wgrad_halo_kernelILi128", "conv3x3_wgrad_halo<128>"),
+    (r"conv3x3_wgrad_halo_kernel<64>|conv3x3_wgrad_halo_kernelILi64", "conv3x3_wgrad_halo<64>"),
+    (r"gemm_gather_kernelIDF16b", "gemm_gather<bf16>"),
+    (r"gemm_gather_kernelIf", "gemm_gather<f32>"),
+    (r"gemm_wgrad_bf16_kernel", "gemm_wgrad_bf16"),
+    (r"gemm_wgrad_kernel", "gemm_wgrad<f32>"),
+]
+
+
+def short(name):
+    for pat, s in NAME_MAP:
+        if re.search(pat, name):
+            return s
+    return name
 
 
 def load(path):
@@ -16,14 +48,14 @@ def load(path):
     return agg, calls, dur
 
 
-if __name__ == "__main__":
-    agg, calls, dur = load(sys.argv[1])
+def report(path, top=12):
+    agg, calls, dur = load(path)
     keys = sorted(agg, key=lambda k: -sum(dur[k].values()))
-    for k in keys[:int(sys.argv[2]) if len(sys.argv) > 2 else 12]:
+    for k in keys[:top]:
         c = agg[k]
         n = len(calls[k])
         t = sum(dur[k].values())
-        line = f"{t / 1e6:8.2f} ms {n:4d} calls {k[:60]:60s}"
+        line = f"{t / 1e6:8.2f} ms {n:4d} calls {short(k)[:40]:40s}"
         if "SQ_WAVE_CYCLES" in c:
             wc = c["SQ_WAVE_CYCLES"]
             line += (f" wait {c['SQ_WAIT_ANY'] / wc:5.2f} waitinst {c['SQ_WAIT_INST_ANY'] / wc:5.2f} "
@@ -36,3 +68,39 @@ if __name__ == "__main__":
             if ctr in c:
                 line += f" {ctr} {c[ctr] * 1024 / n / 1e6:9.1f} MB/call"
         print(line)
+
+
+def traffic(out, fetch_csv, write_csv):
+    fa, fc, fd = load(fetch_csv)
+    wa, wc, wd = load(write_csv)
+    res = {}
+    per = defaultdict(lambda: {"fetch": 0.0, "write": 0.0, "calls_f": 0, "calls_w": 0, "ns": 0})
+    for k in fa:
+        s = short(k)
+        per[s]["fetch"] += fa[k]["FETCH_SIZE"] * 1024 * 2
+        per[s]["calls_f"] += len(fc[k])
+        per[s]["ns"] += sum(fd[k].values())
+    for k in wa:
+        s = short(k)
+        per[s]["write"] += wa[k]["WRITE_SIZE"] * 1024
+        per[s]["calls_w"] += len(wc[k])
+    for s, v in per.items():
+        if v["calls_f"] == 0 or v["calls_w"] == 0:
+            continue
+        f = v["fetch"] / v["calls_f"]
+        w = v["write"] / v["calls_w"]
+        res[s] = {"hbm_bytes_per_launch": f + w, "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
+                  "launches": v["calls_f"], "avg_launch_us": v["ns"] / v["calls_f"] / 1e3}
+    doc = {"method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; "
+                     "bytes = FETCH_SIZE*1024*2 (gfx950 half-count correction) + WRITE_SIZE*1024, per launch",
+           "sources": [fetch_csv, write_csv], "kernels": res}
+    with open(out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(f"wrote {out}: {len(res)} kernels")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--traffic":
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4])
+    else:
+        report(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 12)
