@@ -65,6 +65,52 @@ def train_step(net, opt, x, lab, selective, lamb, chunks=1):
     return res
 
 
+def check_step(d, s, r, strict):
+    """Compare one training step's results `r` (loss, coverage, output, grads, params, buffers,
+    num_batches_tracked — numpy) with step `s` of golden fixture `d`; returns failure strings."""
+    selective = bool(d["meta_selective"])
+    pre = f"s{s}/"
+    tol = 1e-4 if strict else 1e-2
+    ref_loss = float(d[pre + "loss"])
+    assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
+    if selective:
+        assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
+    if pre + "output" in d.files:
+        assert G.max_rel(r["output"], d[pre + "output"]) < tol
+    else:
+        flat = r["output"].ravel()
+        assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol
+    fails = []
+    if strict:
+        mask = O.train_pred_mask(r["output"])  # train.py:150,153
+        if hashlib.sha1(mask.tobytes()).hexdigest() != d[pre + "output_mask_sha1"].item().decode():
+            assert pre + "output" in d.files, "mask hash mismatch"
+            refm = O.train_pred_mask(d[pre + "output"])
+            diff = mask != refm
+            # any flipped pixel must sit within the logit tolerance of the decision boundary
+            assert np.abs(d[pre + "output"][diff]).max() < 1e-4 * np.abs(d[pre + "output"]).max(), diff.sum()
+    if s == 0:
+        # gradients: no worse than the reference's own fp32 error against its fp64 run
+        f, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
+        print("worst grad errors vs fp64 (ours, reference fp32):",
+              [(n, f"{a:.1e}", f"{b:.1e}") for n, a, b in report[:6]])
+        fails += f
+        fails += G.check_tensors(d, pre + "grad", r["grads"], rtol=0.0, atol=1e-6,
+                                 skip=set(r["grads"]) - PRE_BN_BIAS)  # pre-BN biases: ~0
+    # (after one Adam step every element has moved by ~lr*sign(g); elements whose gradient
+    # sits within rounding of zero move either way, so later-step gradients are not compared
+    # element-wise — loss, logits, parameters and BN buffers are, loosely)
+    # Adam moves an element by ~lr*sign(g); elements whose gradient sits at rounding level
+    # (pre-BN biases, near-tie ReLU/max-pool routes) can move the other way: floor 2.5*lr.
+    fails += G.check_tensors(d, pre + "param", r["params"], rtol=1e-5, atol=2.5e-3 if strict else 5e-3)
+    for k, v in r["buffers"].items():
+        if "running" in k:
+            at = 1e-5 if strict else 3e-3
+            np.testing.assert_allclose(v, d[pre + "buf/" + k], rtol=1e-4 if strict else 1e-2, atol=at, err_msg=k)
+    assert int(r["num_batches_tracked"]) == int(d[pre + "num_batches_tracked"])
+    return fails
+
+
 def run_fixture(fname, strict_steps=1):
     d = G.load(fname)
     n, size = int(d["meta_n"]), int(d["meta_size"])
@@ -77,48 +123,11 @@ def run_fixture(fname, strict_steps=1):
     fails = []
     for s in range(int(d["meta_steps"])):
         r = train_step(net, opt, xt, lt, selective, int(d["meta_lamb"]), int(d["meta_chunks"]))
-        pre = f"s{s}/"
-        strict = s < strict_steps
-        tol = 1e-4 if strict else 1e-2
-        ref_loss = float(d[pre + "loss"])
-        assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
-        if selective:
-            assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
-        if pre + "output" in d.files:
-            assert G.max_rel(r["output"], d[pre + "output"]) < tol
-        else:
-            flat = r["output"].ravel()
-            assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol
-        if strict:
-            mask = O.train_pred_mask(r["output"])  # train.py:150,153
-            if hashlib.sha1(mask.tobytes()).hexdigest() != d[pre + "output_mask_sha1"].item().decode():
-                assert pre + "output" in d.files, "mask hash mismatch"
-                refm = O.train_pred_mask(d[pre + "output"])
-                diff = mask != refm
-                # any flipped pixel must sit within the logit tolerance of the decision boundary
-                assert np.abs(d[pre + "output"][diff]).max() < 1e-4 * np.abs(d[pre + "output"]).max(), diff.sum()
-        if s == 0:
-            # gradients: no worse than the reference's own fp32 error against its fp64 run
-            f, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
-            print(f"{fname} worst grad errors vs fp64 (ours, reference fp32):",
-                  [(n, f"{a:.1e}", f"{b:.1e}") for n, a, b in report[:6]])
-            fails += f
-            fails += G.check_tensors(d, pre + "grad", r["grads"], rtol=0.0, atol=1e-6,
-                                     skip=set(r["grads"]) - PRE_BN_BIAS)  # pre-BN biases: ~0
-        # (after one Adam step every element has moved by ~lr*sign(g); elements whose gradient
-        # sits within rounding of zero move either way, so later-step gradients are not compared
-        # element-wise — loss, logits, parameters and BN buffers are, loosely)
-        pv = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
-        # Adam moves an element by ~lr*sign(g); elements whose gradient sits at rounding level
-        # (pre-BN biases, near-tie ReLU/max-pool routes) can move the other way: floor 2.5*lr.
-        fails += G.check_tensors(d, pre + "param", pv, rtol=1e-5, atol=2.5e-3 if strict else 5e-3)
+        r["params"] = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
         bufs = dict(net.named_buffers())
-        for k, v in bufs.items():
-            if "running" in k:
-                at = 1e-5 if strict else 3e-3
-                np.testing.assert_allclose(v.cpu().numpy(), d[pre + "buf/" + k], rtol=1e-4 if strict else 1e-2,
-                                           atol=at, err_msg=k)
-        assert int(bufs["encoder_layer_1_1.1.num_batches_tracked"]) == int(d[pre + "num_batches_tracked"])
+        r["buffers"] = {k: v.cpu().numpy() for k, v in bufs.items()}
+        r["num_batches_tracked"] = int(bufs["encoder_layer_1_1.1.num_batches_tracked"])
+        fails += check_step(d, s, r, strict=s < strict_steps)
     assert not fails, "\n".join(fails[:25])
 
 
