@@ -247,6 +247,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
             "final_loss": round(final_loss, 5),
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
