@@ -11,6 +11,8 @@
 // chunk's first six taps (load early, write late) into the second halo buffer.
 // LDS rows are 144 B (128 B + 16 B pad) so ds_read_b128 fragment reads of 16 consecutive rows hit
 // 16 distinct bank slots.
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace selunet {
@@ -21,8 +23,11 @@ constexpr int HPIX = HHT * HWT;         // 324 halo pixels
 constexpr int HTHREADS = 512;
 constexpr int A_ROUNDS = (HPIX * 8 + HTHREADS - 1) / HTHREADS;  // 16-B halo loads per thread per chunk
 
-template <typename T, int BN>
-__global__ void __launch_bounds__(HTHREADS, 2)
+// ONE_CHUNK: the whole K of a tap fits one chunk (C == CK): a single halo buffer, no halo
+// prefetch, and LDS small enough for two workgroups per CU so one's prologue/epilogue overlaps
+// the other's MFMAs.
+template <typename T, int BN, bool ONE_CHUNK>
+__global__ void __launch_bounds__(HTHREADS, ONE_CHUNK ? 2 : 1)
 conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int tiles_x,
                     int tiles_y) {
   constexpr int E = 16 / sizeof(T);       // elements per 16-B vector
@@ -32,12 +37,18 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
   constexpr int WPIX = (TH * TW) / WAVES_M;  // 64 or 32 pixels per wave
   constexpr int MT = WPIX / 32;
   constexpr int NT = 2;                   // 64 channels per wave
-  constexpr int B_ROUNDS = (BN * 8 + HTHREADS - 1) / HTHREADS;
+  constexpr int B_ROUNDS = BN * 8 / HTHREADS;
+  static_assert(B_ROUNDS * HTHREADS == BN * 8, "weight tile rows must split evenly over the threads");
+  constexpr int NHBUF = ONE_CHUNK ? 1 : 2;
+  constexpr int AD = 3;                   // halo slice loaded at tap r is written at tap r + AD
 
-  constexpr int SMEM_MAIN = 2 * HPIX * ROWB + 2 * BN * ROWB, SMEM_EPI = TH * TW * (BN + 4) * 4;
+  constexpr int SMEM_MAIN = NHBUF * HPIX * ROWB + 2 * BN * ROWB + (ONE_CHUNK ? 0 : 2 * CK * 8);
+  constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
   unsigned char* As = smem;
-  unsigned char* Bs = smem + 2 * HPIX * ROWB;
+  unsigned char* Bs = smem + NHBUF * HPIX * ROWB;
+  // folded BN coefficients of the prefetched chunk: [2 buffers][CK] scale, then [2][CK] shift
+  float* Ss = reinterpret_cast<float*>(Bs + 2 * BN * ROWB);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -58,58 +69,51 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
   const int nsteps = nchunks * 9;
 
   // ---------------------------------------------------------------- staging helpers
-  uint4 ra;
-  bool aok;
-  int a_s = 0, a_c = 0;
-  auto a_load = [&](int chunk, int round) {
+  // halo slice `round` of this thread: halo pixel hp, 16-B column cc; false outside the slice
+  // (hp clamped into the tile for the partial last round, so loads can be issued unconditionally)
+  auto a_slot = [&](int round, int& hp, int& cc) -> bool {
     const int hidx = round * HTHREADS + tid;
-    aok = false;
-    ra = make_uint4(0, 0, 0, 0);
-    if (hidx >= HPIX * 8) return;
-    const int hp = hidx >> 3, cc = hidx & 7;
-    const int hy = hp / HWT, hx = hp - hy * HWT;
-    const int ys = y0 - 1 + hy, xs = x0 - 1 + hx;
+    hp = min(hidx >> 3, HPIX - 1);
+    cc = hidx & 7;
+    return hidx < HPIX * 8;
+  };
+  auto a_inside = [&](int hp) -> bool {
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    return (unsigned)(y0 - 1 + hy) < (unsigned)g.h && (unsigned)(x0 - 1 + hx) < (unsigned)g.w;
+  };
+  // global address of chunk `chunk`'s 16-B slice (hp, cc), the pixel clamped into the image (the
+  // zero padding is applied when the slice is written to LDS); a chunk never straddles sources
+  auto a_ptr = [&](int chunk, int hp, int cc) -> const uint4* {
     int c = chunk * CK;
-    int s = 0;
-    if (g.nsrc > 1 && c >= g.src[0].C) {
-      c -= g.src[0].C;
-      s = 1;
-    }
-    a_s = s;
-    a_c = c + cc * E;
-    if ((unsigned)ys < (unsigned)g.h && (unsigned)xs < (unsigned)g.w) {
-      const SrcArg sa = pick_src(g, s);
-      ra = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
-                                          (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + a_c);
-      aok = true;
-    }
+    const bool s1 = g.nsrc > 1 && c >= g.src[0].C;
+    if (s1) c -= g.src[0].C;
+    const SrcArg sa = pick_src(g, s1 ? 1 : 0);
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    const int ys = min(max(y0 - 1 + hy, 0), g.h - 1), xs = min(max(x0 - 1 + hx, 0), g.w - 1);
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
+                                          (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + c + cc * E);
   };
-  auto a_store = [&](int buf, int round) {
-    const int hidx = round * HTHREADS + tid;
-    if (hidx >= HPIX * 8) return;
-    const int hp = hidx >> 3, cc = hidx & 7;
-    const SrcArg sa = pick_src(g, a_s);
-    uint4 v = ra;
-    if (sa.scale) v = aok ? transform16<T>(v, sa.scale, sa.shift, a_c, sa.relu) : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(As + (buf * HPIX + hp) * ROWB + cc * 16) = v;
+  struct BRegs {
+    uint4 v[B_ROUNDS];
   };
-  uint4 rb[B_ROUNDS];
-  auto b_load = [&](int step) {
+  auto b_load = [&](int step) __attribute__((always_inline)) {
     const int chunk = step / 9, tap = step - chunk * 9;
     const int k0 = tap * g.Ctot + chunk * CK;
+    BRegs rb;
 #pragma unroll
     for (int r = 0; r < B_ROUNDS; ++r) {
       const int idx = r * HTHREADS + tid;
       const int row = idx >> 3, cc = idx & 7;
-      if (row < BN) rb[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
+      rb.v[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
     }
+    return rb;
   };
-  auto b_store = [&](int buf) {
+  auto b_store = [&](const BRegs& rb, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < B_ROUNDS; ++r) {
       const int idx = r * HTHREADS + tid;
       const int row = idx >> 3, cc = idx & 7;
-      if (row < BN) *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb[r];
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb.v[r];
     }
   };
 
@@ -127,25 +131,9 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     hrow0[a] = (pix / TW) * HWT + (pix % TW);
   }
 
-  // ---------------------------------------------------------------- prologue
-  for (int r = 0; r < A_ROUNDS; ++r) {
-    a_load(0, r);
-    a_store(0, r);
-  }
-  b_load(0);
-  b_store(0);
-  __syncthreads();
-
-  // ---------------------------------------------------------------- main loop
-  for (int s = 0; s < nsteps; ++s) {
-    const int c = s / 9, t = s - (s / 9) * 9;
-    const bool more_b = s + 1 < nsteps;
-    const bool do_a = (c + 1 < nchunks) && (t < A_ROUNDS);
-    if (more_b) b_load(s + 1);
-    if (do_a) a_load(c + 1, t);
-
-    const unsigned char* a_src = As + (c & 1) * HPIX * ROWB;
-    const unsigned char* b_src = Bs + (s & 1) * BN * ROWB;
+  auto mma_step = [&](int hbuf, int bbuf, int t) __attribute__((always_inline)) {
+    const unsigned char* a_src = As + hbuf * HPIX * ROWB;
+    const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
 #pragma unroll
@@ -162,9 +150,99 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
 #pragma unroll
         for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
     }
-    if (more_b) b_store((s + 1) & 1);
-    if (do_a) a_store((c + 1) & 1, t);
-    __syncthreads();
+  };
+
+  // ---------------------------------------------------------------- prologue: chunk 0, B(0), B(1)
+  {
+    const int c0 = 0;
+    const SrcArg sa = pick_src(g, 0);
+    uint4 v0[A_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) {
+      int hp, cc;
+      a_slot(r, hp, cc);
+      v0[r] = *a_ptr(0, hp, cc);
+    }
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) {
+      int hp, cc;
+      if (!a_slot(r, hp, cc)) continue;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (a_inside(hp)) {
+        v = v0[r];
+        if (sa.scale) v = transform16<T>(v, sa.scale, sa.shift, c0 + cc * E, sa.relu);
+      }
+      *reinterpret_cast<uint4*>(As + hp * ROWB + cc * 16) = v;
+    }
+  }
+  BRegs rb_next = b_load(0);
+  b_store(rb_next, 0);
+  rb_next = b_load(nsteps > 1 ? 1 : 0);
+  __syncthreads();
+
+  if constexpr (ONE_CHUNK) {
+    // ------------------------------------------------------------ 9 taps of the single chunk
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      BRegs rb_far = rb_next;
+      if (t + 2 < 9) rb_far = b_load(t + 2);
+      mma_step(0, t & 1, t);
+      if (t + 1 < 9) b_store(rb_next, (t + 1) & 1);
+      __syncthreads();
+      rb_next = rb_far;
+    }
+  } else {
+    // ------------------------------------------------------------ main loop over chunks
+    uint4 ra[A_ROUNDS];
+    for (int c = 0; c < nchunks; ++c) {
+      const int cn = c + 1 < nchunks ? c + 1 : c;  // prefetched chunk (the last one reloads itself)
+      int cs = cn * CK;
+      const bool s1 = g.nsrc > 1 && cs >= g.src[0].C;
+      if (s1) cs -= g.src[0].C;
+      const SrcArg sn = pick_src(g, s1 ? 1 : 0);
+      float* ssc = Ss + ((c + 1) & 1) * CK;
+      float* ssh = Ss + 2 * CK + ((c + 1) & 1) * CK;
+      float coef = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int s = c * 9 + t;
+        const BRegs rb_far = b_load(s + 2 < nsteps ? s + 2 : nsteps - 1);
+        if (t == 0 && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
+        if (t < A_ROUNDS) {
+          int hp, cc;
+          a_slot(t, hp, cc);
+          ra[t] = *a_ptr(cn, hp, cc);
+        }
+        mma_step(c & 1, s & 1, t);
+        b_store(rb_next, (s + 1) & 1);
+        if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
+        if (t >= AD && t - AD < A_ROUNDS) {
+          const int r = t - AD;
+          int hp, cc;
+          if (a_slot(r, hp, cc)) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (a_inside(hp)) {
+              v = ra[r];
+              if (sn.scale) {
+                // transform with the coefficients staged in LDS at t == 1 (visible after its barrier)
+                T e[E];
+                __builtin_memcpy(e, &v, 16);
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                  float f = to_f(e[j]) * ssc[cc * E + j] + ssh[cc * E + j];
+                  if (sn.relu) f = fmaxf(f, 0.0f);
+                  e[j] = from_f<T>(f);
+                }
+                __builtin_memcpy(&v, e, 16);
+              }
+            }
+            *reinterpret_cast<uint4*>(As + (((c + 1) & 1) * HPIX + hp) * ROWB + cc * 16) = v;
+          }
+        }
+        __syncthreads();
+        rb_next = rb_far;
+      }
+    }
   }
 
   // ---------------------------------------------------------------- epilogue (LDS-staged)
@@ -400,13 +478,17 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
   const int n_tiles = N / BN;
   const int64_t blocks = conv3x3_halo_tiles(g) * n_tiles;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<T, BN>), dim3((unsigned)blocks), dim3(HTHREADS), 0, st, g,
-                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y);
+  const bool one = g.Ctot == 128 / (int)sizeof(T);
+  auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N, k_pad,
+                     ep, n_tiles, tiles_x, tiles_y);
 }
 
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st) {
-  const bool bn128 = N % 128 == 0 && !(ep.mode == SELUNET_EP_SPLIT && ep.split % 128 != 0);
+  // single-chunk layers use 64-column tiles: LDS for two workgroups per CU
+  const bool one = g.Ctot == (dtype == SELUNET_F32 ? 32 : 64);
+  const bool bn128 = !one && N % 128 == 0 && !(ep.mode == SELUNET_EP_SPLIT && ep.split % 128 != 0);
   if (dtype == SELUNET_F32) {
     if (bn128) launch_halo<float, 128>(g, b, N, k_pad, ep, st);
     else launch_halo<float, 64>(g, b, N, k_pad, ep, st);
