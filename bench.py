@@ -68,6 +68,7 @@ class KernelTimer:
         self.active = False
         self.esz = esz
         self.rec = {}  # kernel name -> list of (start, end, flops, bytes)
+        self.shapes = {}  # (kernel name, operand shape) -> list of (start, end, flops)
 
     @staticmethod
     def _k(g):
@@ -87,17 +88,28 @@ class KernelTimer:
             m = g.n * g.h * g.w
             flops = 2.0 * m * n_cols * self._k(g)
             nbytes = self._src_bytes(g) + m * n_cols * self.esz + n_cols * self._k(g) * self.esz
+            shape = f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
         else:
             gp, gq = args[0], args[1]
             kname = K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, args[3]).decode()
             flops = 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
+            shape = f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         rc = fn()
         e.record()
         self.rec.setdefault(kname, []).append((s, e, flops, nbytes))
+        self.shapes.setdefault((kname, shape), []).append((s, e, flops))
         return rc
+
+    def shape_summary(self, steps):
+        rows = []
+        for (k, shape), lst in self.shapes.items():
+            ms = sum(s.elapsed_time(e) for s, e, _ in lst)
+            fl = sum(f for _, _, f in lst)
+            rows.append((ms / steps, k, shape, len(lst) // steps, fl / (ms * 1e-3) / 1e12 if ms else 0.0))
+        return sorted(rows, reverse=True)
 
     def summary(self):
         out = {}
@@ -229,7 +241,8 @@ def main():
                             "hbm_gbs_algorithmic": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else 0.0}
                         for n, v in sorted(ksum.items(), key=lambda kv: -kv[1]["ms"])}}
         if args.layer_report and rank == 0:
-            print(json.dumps(roof, indent=1), file=sys.stderr)
+            for ms, k, shape, n, tf in timer.shape_summary(args.steps):
+                print(f"{ms:7.3f} ms/step {n:2d}x {tf:7.1f} TF/s  {k:26s} {shape}", file=sys.stderr)
     whole = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * value / 1e3  # TFLOP/s whole step
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

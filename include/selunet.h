@@ -76,6 +76,19 @@ enum { SELUNET_EP_PLAIN = 0, SELUNET_EP_SPLIT = 1, SELUNET_EP_SCATTER2X = 2 };
  * (ConvTranspose2d k2 s2 forward). bias (fp32, per output channel) is added when
  * non-NULL. stats (fp32 [selunet_gemm_stats_rows(a, N, dtype)][2][N]): per-workgroup column
  * sum and sum of squares of the fp32 accumulators (BatchNorm batch statistics, model.py:12). */
+/* BatchNorm-backward partial sums of a freshly written data gradient dA of a CBR block (fused into
+ * the kernel that produces dA instead of re-reading it): per workgroup and channel,
+ * sum(da), sum(da*xhat), sum(xhat) with da = dA*[y*scale+shift > 0], xhat = (y-mean)*invstd,
+ * dA rounded to the activation dtype first (as stored). slab = NULL disables it. */
+typedef struct selunet_bn_bwd_stats {
+  const void* y;       /* the block's pre-BN conv output, same [M][C] layout as dA */
+  const float* scale;  /* folded BN + ReLU of the forward pass */
+  const float* shift;
+  const float* mean;   /* batch statistics of the forward pass */
+  const float* invstd;
+  float* slab;         /* [rows][3][C] */
+} selunet_bn_bwd_stats;
+
 typedef struct selunet_epilogue {
   void* out0;
   void* out1;
@@ -83,6 +96,11 @@ typedef struct selunet_epilogue {
   float* stats;
   int32_t mode;
   int32_t split;
+  /* SPLIT only (nullable): [stats_rows][split] per-workgroup column sums of the out0 part (the
+   * ConvTranspose2d bias gradient of the up-sampled half of a torch.cat, model.py:44,51,57). */
+  float* colsum;
+  /* PLAIN only: BatchNorm-backward sums of the written tile, slab [stats_rows][3][N]. */
+  selunet_bn_bwd_stats bnb;
 } selunet_epilogue;
 
 const char* selunet_last_error(void);
@@ -167,20 +185,26 @@ int selunet_im2col3x3(const float* x, int32_t n, int32_t c, int32_t h, int32_t w
 int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
                          const float* scale, const float* shift, void* out, int32_t dtype,
                          void* stream);
-/* dz = route(dpool to the first max of each window, row-major, strict >) + dskip (nullable). */
+/* dz = route(dpool to the first max of each window, row-major, strict >) + dskip (nullable).
+ * bnb (nullable; bnb->y must be y): BatchNorm-backward sums of dz, slab
+ * [selunet_maxpool2_bwd_slab_rows(n, h, w, c)][3][c]. */
 int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
                          const float* scale, const float* shift, const void* dpool,
-                         const void* dskip, void* dz, int32_t dtype, void* stream);
+                         const void* dskip, void* dz, const selunet_bn_bwd_stats* bnb, int32_t dtype,
+                         void* stream);
+int64_t selunet_maxpool2_bwd_slab_rows(int32_t n, int32_t h, int32_t w, int32_t c);
 
 /* ---- 1x1 heads conv1x1 / conv_select / conv_aux on relu(bn(y)), C = 64 (model.py:62-66) */
 int selunet_heads_fwd(const void* y, int64_t m, const float* scale, const float* shift,
                       const float* w, const float* b, int32_t nh, float* out0, float* out1,
                       float* out2, int32_t dtype, void* stream);
 /* dz[m][c] = sum_h g_h[m] w_h[c]; slab [selunet_channel_slab_rows(M)][nh][65]: per head
- * sum g*z (weight grad, 64) and sum g (bias grad). */
+ * sum g*z (weight grad, 64) and sum g (bias grad). bnb (nullable; bnb->y must be y):
+ * BatchNorm-backward sums of dz, slab [selunet_channel_slab_rows(M)][3][64]. */
 int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float* shift,
                       const float* w, int32_t nh, const float* g0, const float* g1,
-                      const float* g2, void* dz, float* slab, int32_t dtype, void* stream);
+                      const float* g2, void* dz, float* slab, const selunet_bn_bwd_stats* bnb,
+                      int32_t dtype, void* stream);
 
 /* ---- losses ----------------------------------------------------------------------------- */
 /* calc_selective_risk_image_b (selective_loss.py:58-85), numerically stable form.

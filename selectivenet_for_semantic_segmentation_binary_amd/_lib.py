@@ -33,9 +33,14 @@ class Gather(ctypes.Structure):
                 ("reserved", c_int32), ("src", Source * 2)]
 
 
+class BnBwdStats(ctypes.Structure):
+    _fields_ = [("y", c_void_p), ("scale", c_void_p), ("shift", c_void_p), ("mean", c_void_p),
+                ("invstd", c_void_p), ("slab", c_void_p)]
+
+
 class Epilogue(ctypes.Structure):
     _fields_ = [("out0", c_void_p), ("out1", c_void_p), ("bias", c_void_p), ("stats", c_void_p),
-                ("mode", c_int32), ("split", c_int32)]
+                ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats)]
 
 
 class AdamTensor(ctypes.Structure):
@@ -70,9 +75,12 @@ SIGNATURES = {
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),
     "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
-    "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P,
+                                       ctypes.POINTER(BnBwdStats), c_int32, P]),
+    "selunet_maxpool2_bwd_slab_rows": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
     "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),
-    "selunet_heads_bwd": (c_int32, [P, c_int64, P, P, P, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_heads_bwd": (c_int32, [P, c_int64, P, P, P, c_int32, P, P, P, P, P, ctypes.POINTER(BnBwdStats),
+                                    c_int32, P]),
     "selunet_loss_slab_rows": (c_int64, [c_int64]),
     "selunet_selective_partials": (c_int32, [P, P, P, c_int64, P, P]),
     "selunet_selective_finalize": (c_int32, [P, c_double, c_float, c_float, P, P, P, P]),

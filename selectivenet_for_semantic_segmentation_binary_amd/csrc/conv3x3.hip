@@ -260,8 +260,7 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     return reinterpret_cast<T*>(ep.out0) + m * N + col;
   };
   auto bias_col = [&](int c) { return n0 + c; };
-  float* st = ep.stats ? ep.stats + ((int64_t)ptile * 2) * N + n0 : nullptr;
-  lds_tile_store<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, st, N);
+  lds_tile_store<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, ptile, n0, N));
 }
 
 // =========================================================================== weight gradient
@@ -323,58 +322,84 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
   const SrcArg& pa = P.src[0];
   const int H = P.h, W = P.w;
 
+  // folded BN coefficients of the block's dY and X channels, staged once in LDS and applied when a
+  // tile is written to LDS (the raw loads stay in flight across the previous tile's MFMAs)
+  __shared__ float Ks[2 * BI + 2 * 64];
+  if (tid < 2 * BI + 128) {
+    float v;
+    if (tid < 2 * BI) {
+      const int c = i0 + (tid % BI);
+      v = pa.scale ? (tid < BI ? pa.scale[c] : pa.shift[c]) : 0.0f;
+    } else {
+      const int c = xc + ((tid - 2 * BI) % 64);
+      v = xa.scale ? (tid < 2 * BI + 64 ? xa.scale[c] : xa.shift[c]) : 0.0f;
+    }
+    Ks[tid] = v;
+  }
+
+  auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
+    x0 = ((unsigned)pt - r2 * (unsigned)tiles_x) * WTW;
+    const unsigned r3 = r2 / (unsigned)tiles_y;
+    y0 = (r2 - r3 * (unsigned)tiles_y) * WTH;
+    img = (int)r3;
+  };
+  auto apply = [&](uint4 v, const float* sc, const float* sh, int relu) __attribute__((always_inline)) {
+    __bf16 e[8];
+    __builtin_memcpy(e, &v, 16);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)e[j] * sc[j] + sh[j];
+      if (relu) f = fmaxf(f, 0.0f);
+      e[j] = (__bf16)f;
+    }
+    __builtin_memcpy(&v, e, 16);
+    return v;
+  };
+  // unconditional loads (pixels clamped into the image; zeroed when written), so the compiler can
+  // count the outstanding loads instead of waiting for each one
   uint4 rp[P_ROUNDS], rx[X_ROUNDS];
-  bool xok[X_ROUNDS];
-  auto load_tile = [&](int64_t pt) {
-    const int tx = (int)(pt % tiles_x);
-    const int64_t r2 = pt / tiles_x;
-    const int ty = (int)(r2 % tiles_y);
-    const int img = (int)(r2 / tiles_y);
-    const int y0 = ty * WTH, x0 = tx * WTW;
+  auto load_tile = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
       const int idx = r * 512 + tid;
       const int px = idx / (BI / 8), cc = idx % (BI / 8);
-      const int y = y0 + px / WTW, x = x0 + px % WTW;
-      rp[r] = make_uint4(0, 0, 0, 0);
-      if (y < H && x < W) {
-        const int c = i0 + cc * 8;
-        rp[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(pa.data) +
-                                               (((int64_t)img * H + y) * W + x) * pa.C + c);
-        if (pa.scale) rp[r] = transform16<__bf16>(rp[r], pa.scale, pa.shift, c, pa.relu);
-      }
+      const int y = min(y0 + px / WTW, H - 1), x = min(x0 + px % WTW, W - 1);
+      rp[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(pa.data) +
+                                             (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 8);
     }
 #pragma unroll
     for (int r = 0; r < X_ROUNDS; ++r) {
       const int idx = r * 512 + tid;
-      rx[r] = make_uint4(0, 0, 0, 0);
-      xok[r] = false;
+      const int hp = min(idx >> 3, WHP - 1), cc = idx & 7;
+      const int y = min(max(y0 - 1 + hp / WHW, 0), H - 1), x = min(max(x0 - 1 + hp % WHW, 0), W - 1);
+      rx[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(xa.data) +
+                                             (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 8);
+    }
+  };
+  auto store_tile = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 8), cc = idx % (BI / 8);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (y0 + px / WTW < H && x0 + px % WTW < W)
+        v = pa.scale ? apply(rp[r], Ks + cc * 8, Ks + BI + cc * 8, pa.relu) : rp[r];
+      *reinterpret_cast<uint4*>(&Ps[buf][px][cc * 8]) = v;
+    }
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
       if (idx < WHP * 8) {
         const int hp = idx >> 3, cc = idx & 7;
         const int y = y0 - 1 + hp / WHW, x = x0 - 1 + hp % WHW;
-        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
-          rx[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(xa.data) +
-                                                 (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 8);
-          xok[r] = true;
-        }
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < P_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
-      const int px = idx / (BI / 8), cc = idx % (BI / 8);
-      *reinterpret_cast<uint4*>(&Ps[buf][px][cc * 8]) = rp[r];
-    }
-#pragma unroll
-    for (int r = 0; r < X_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
-      if (idx < WHP * 8) {
-        const int hp = idx >> 3, cc = idx & 7;
-        uint4 v = rx[r];
-        if (xa.scale) v = xok[r] ? transform16<__bf16>(v, xa.scale, xa.shift, xc + cc * 8, xa.relu)
-                                 : make_uint4(0, 0, 0, 0);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          v = xa.scale ? apply(rx[r], Ks + 2 * BI + cc * 8, Ks + 2 * BI + 64 + cc * 8, xa.relu) : rx[r];
         *reinterpret_cast<uint4*>(&Xs[buf][hp][cc * 8]) = v;
       }
     }
@@ -384,13 +409,15 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
 #pragma unroll
   for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
 
-  load_tile(pt_begin);
-  store_tile(0);
+  load_tile((int)pt_begin);
+  __syncthreads();  // coefficients visible
+  store_tile((int)pt_begin, 0);
   __syncthreads();
   int buf = 0;
-  for (int64_t pt = pt_begin; pt < pt_end; ++pt) {
-    const bool more = pt + 1 < pt_end;
-    if (more) load_tile(pt + 1);
+  for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+    const bool more = pt + 1 < (int)pt_end;
+    load_tile(more ? pt + 1 : pt);
+    __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
 #pragma unroll
     for (int ks = 0; ks < WTH; ++ks) {   // one tile row (16 pixels) per k-step
       const int prow = ks * WTW + 8 * half + q4;
@@ -412,7 +439,7 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
         }
       }
     }
-    if (more) store_tile(buf ^ 1);
+    if (more) store_tile(pt + 1, buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }

@@ -210,8 +210,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
            ((img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + cq;
   };
   auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
-  float* st = ep.stats ? ep.stats + (m_tile * 2) * N + n0 : nullptr;
-  lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, st, N);
+  lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, m_tile, n0, N));
 }
 
 // =========================================================================== gemm_wgrad
@@ -662,7 +661,14 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
   if (ep->mode == SELUNET_EP_SCATTER2X)
     SELUNET_REQUIRE(n_cols % 4 == 0 && a->taps == 1, "scatter2x epilogue needs taps == 1 and n_cols % 4 == 0");
   SELUNET_REQUIRE(ep->stats == nullptr || ep->mode == SELUNET_EP_PLAIN, "stats only with the plain epilogue");
-  EpiArg e{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split};
+  SELUNET_REQUIRE(ep->colsum == nullptr || ep->mode == SELUNET_EP_SPLIT, "colsum only with the split epilogue");
+  const selunet_bn_bwd_stats& bb = ep->bnb;
+  if (bb.slab != nullptr)
+    SELUNET_REQUIRE(ep->mode == SELUNET_EP_PLAIN && ep->stats == nullptr && bb.y && bb.scale && bb.shift && bb.mean &&
+                        bb.invstd && ep->bias == nullptr,
+                    "bn-backward sums need the plain epilogue without stats/bias and y/scale/shift/mean/invstd");
+  EpiArg e{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split, ep->colsum,
+           BnBwdArg{bb.y, bb.scale, bb.shift, bb.mean, bb.invstd, bb.slab}};
   hipStream_t st = as_stream(stream);
   if (ep->mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype))
     return conv3x3_halo_launch(g, b, n_cols, k_pad, e, dtype, st);

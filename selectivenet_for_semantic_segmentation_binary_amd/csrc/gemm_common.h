@@ -153,6 +153,15 @@ __device__ __forceinline__ uint4 transform16(uint4 raw, const float* scale, cons
 }
 
 // =========================================================================== gemm_gather
+struct BnBwdArg {
+  const void* y;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  float* slab;
+};
+
 struct EpiArg {
   void* out0;
   void* out1;
@@ -160,6 +169,8 @@ struct EpiArg {
   float* stats;
   int mode;
   int split;
+  float* colsum;
+  BnBwdArg bnb;
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -189,14 +200,49 @@ __device__ __forceinline__ void acc_to_lds(float* tile, const f32x16 (&acc)[MT][
         tile[(wr0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * (TC + 4) + wc0 + b * 32 + l32] = acc[a][b][r];
 }
 
+// Per-workgroup statistics an epilogue can produce while it stores its tile (all optional):
+//  stats  [2][ld]      column sum / sum of squares of the fp32 values before the bias (BN forward);
+//  colsum [ld_colsum]  column sums of the stored values for global columns < colsum_cols (SPLIT:
+//                      the ConvTranspose2d bias gradient of out0's half);
+//  bnb                 BN-backward sums [3][ld] of the stored values as dA (PLAIN): y is read at the
+//                      element the value is stored to (same [M][N] layout), da = dA*[y*sc+sh > 0],
+//                      sums (da, da*xhat, xhat); the pointers are offset to the tile's first column.
+struct TileStats {
+  float* stats;
+  int ld;
+  float* colsum;
+  int colsum_cols;     // global column bound for colsum
+  int gcol0;           // global column of tile column 0
+  BnBwdArg bnb;        // scale/shift/mean/invstd/slab offset to gcol0; y = base pointer
+  const void* out0;    // base of the PLAIN output (to locate y)
+};
+
+// The statistics outputs of workgroup (slab row `row`, first global column n0) of an N-column GEMM.
+__device__ __forceinline__ TileStats tile_stats(const EpiArg& ep, int64_t row, int n0, int N) {
+  TileStats ts;
+  ts.ld = N;
+  ts.stats = ep.stats ? ep.stats + row * 2 * N + n0 : nullptr;
+  ts.colsum = ep.colsum ? ep.colsum + row * ep.split + n0 : nullptr;
+  ts.colsum_cols = ep.split;
+  ts.gcol0 = n0;
+  ts.bnb = ep.bnb;
+  if (ep.bnb.slab) {
+    ts.bnb.scale += n0;
+    ts.bnb.shift += n0;
+    ts.bnb.mean += n0;
+    ts.bnb.invstd += n0;
+    ts.bnb.slab += row * 3 * N + n0;
+  }
+  ts.out0 = ep.out0;
+  return ts;
+}
+
 // Store the LDS tile as 8-column vectors (16 B bf16 / 32 B fp32): dst(row, col) returns the
 // global address of tile element (row, col) (col a multiple of 8) or nullptr for a masked row.
-// bias (nullable) is indexed by bias_col(col). If stats != nullptr, per-column sum / sum of
-// squares over the stored rows (before the bias) go to stats[0][col], stats[1][col] of the
-// block's slab row (stride ld_stats between the two).
+// bias (nullable) is indexed by bias_col(col).
 template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
 __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
-                                      float* stats, int ld_stats) {
+                                               const TileStats& ts) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass
   const int cc = tid % CC, r0 = tid / CC;
@@ -204,14 +250,27 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
   float bv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[bias_col(col + e)] : 0.0f;
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool do_st = ts.stats != nullptr;
+  const bool do_cs = ts.colsum != nullptr && ts.gcol0 + col < ts.colsum_cols;
+  const bool do_bn = ts.bnb.slab != nullptr;
+  float sc[8], sh[8], mu[8], is[8];
+  if (do_bn) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = ts.bnb.scale[col + e];
+      sh[e] = ts.bnb.shift[col + e];
+      mu[e] = ts.bnb.mean[col + e];
+      is[e] = ts.bnb.invstd[col + e];
+    }
+  }
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(tile + row * (TC + 4) + col);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(tile + row * (TC + 4) + col + 4);
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    if (stats) {
+    if (do_st) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         s1[e] += v[e];
@@ -220,10 +279,10 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += bv[e];
-    if constexpr (sizeof(T) == 2) {
-      T o[8];
+    T o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = from_f<T>(v[e]);
+    for (int e = 0; e < 8; ++e) o[e] = from_f<T>(v[e]);
+    if constexpr (sizeof(T) == 2) {
       uint4 u;
       __builtin_memcpy(&u, o, 16);
       *reinterpret_cast<uint4*>(p) = u;
@@ -231,24 +290,50 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
       *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
       *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
+    if (do_cs) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s1[e] += to_f(o[e]);
+    }
+    if (do_bn) {
+      const T* yp = reinterpret_cast<const T*>(ts.bnb.y) + (p - reinterpret_cast<const T*>(ts.out0));
+      T yv[8];
+      if constexpr (sizeof(T) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4*>(yp);
+        __builtin_memcpy(yv, &u, 16);
+      } else {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(yp), b = *reinterpret_cast<const f32x4*>(yp + 4);
+        __builtin_memcpy(yv, &a, 16);
+        __builtin_memcpy(yv + 4, &b, 16);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float y = to_f(yv[e]);
+        const float da = y * sc[e] + sh[e] > 0.0f ? to_f(o[e]) : 0.0f;
+        const float xh = (y - mu[e]) * is[e];
+        s1[e] += da;
+        s2[e] += da * xh;
+        s3[e] += xh;
+      }
+    }
   }
-  if (stats) {
+  const int nst = do_bn ? 3 : (do_st ? 2 : 1);
+  if (do_st || ts.colsum != nullptr || do_bn) {
     __syncthreads();  // everyone is done reading the tile: reuse it for the column reduction
-    float* red = tile;  // [RS][TC][2]
+    float* red = tile;  // [RS][TC][3]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[(r0 * TC + col + e) * 2 + 0] = s1[e];
-      red[(r0 * TC + col + e) * 2 + 1] = s2[e];
+      red[(r0 * TC + col + e) * 3 + 0] = s1[e];
+      red[(r0 * TC + col + e) * 3 + 1] = s2[e];
+      red[(r0 * TC + col + e) * 3 + 2] = s3[e];
     }
     __syncthreads();
-    for (int c = tid; c < TC; c += NTHREADS) {
-      float a = 0.0f, b = 0.0f;
-      for (int r = 0; r < RS; ++r) {
-        a += red[(r * TC + c) * 2 + 0];
-        b += red[(r * TC + c) * 2 + 1];
-      }
-      stats[c] = a;
-      stats[ld_stats + c] = b;
+    for (int i = tid; i < TC * nst; i += NTHREADS) {
+      const int c = i % TC, k = i / TC;
+      float a = 0.0f;
+      for (int r = 0; r < RS; ++r) a += red[(r * TC + c) * 3 + k];
+      if (do_bn) ts.bnb.slab[k * ts.ld + c] = a;
+      else if (do_st) ts.stats[k * ts.ld + c] = a;
+      else if (ts.gcol0 + c < ts.colsum_cols) ts.colsum[c] = a;
     }
   }
 }

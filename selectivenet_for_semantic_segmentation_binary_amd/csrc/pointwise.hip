@@ -351,35 +351,63 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ y, int n, int h, int w,
   }
 }
 
+// BN-backward partial sums of dA (channel group c of 4): sum da, sum da*xhat, sum xhat with
+// da = dA*[y*scale+shift > 0] (see selunet_bn_bwd_stats)
+struct BnbAcc {
+  f32x4 acc[3] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  __device__ inline void add(const f32x4& y, const f32x4& da_raw, const f32x4& sc, const f32x4& sh, const f32x4& mu,
+                             const f32x4& is) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float da = y[e] * sc[e] + sh[e] > 0.0f ? da_raw[e] : 0.0f;
+      const float xh = (y[e] - mu[e]) * is[e];
+      acc[0][e] += da;
+      acc[1][e] += da * xh;
+      acc[2][e] += xh;
+    }
+  }
+};
+
+// dz = route(dp) + dskip per 2x2 window; with bnb, the BN-backward sums of dz (as stored) too.
+// Each thread keeps one 4-channel group (the grid stride is a multiple of C/4), so its sums are
+// reduced per block into slab row blockIdx.x.
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w, int C, const float* scale,
                                    const float* shift, const T* __restrict__ dp, const T* __restrict__ dskip,
-                                   T* __restrict__ dz) {
+                                   T* __restrict__ dz, const float* mean, const float* invstd, float* bn_slab) {
   const int ho = h >> 1, wo = w >> 1;
-  const int64_t nv = (int64_t)n * ho * wo * (C / 4);
+  const int CG = C >> 2;
+  const int64_t nv = (int64_t)n * ho * wo * CG;
+  const int c = (int)(threadIdx.x % CG) * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+  f32x4 mu = f32x4{0, 0, 0, 0}, is = f32x4{0, 0, 0, 0};
+  if (bn_slab) {
+    mu = *reinterpret_cast<const f32x4*>(mean + c);
+    is = *reinterpret_cast<const f32x4*>(invstd + c);
+  }
+  BnbAcc bn;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % (C / 4)) * 4;
-    int64_t p = i / (C / 4);
-    const int xo = (int)(p % wo);
-    p /= wo;
-    const int yo = (int)(p % ho);
-    const int64_t img = p / ho;
-    const int64_t off[4] = {((img * h + 2 * yo) * w + 2 * xo) * C + c, ((img * h + 2 * yo) * w + 2 * xo + 1) * C + c,
-                            ((img * h + 2 * yo + 1) * w + 2 * xo) * C + c,
-                            ((img * h + 2 * yo + 1) * w + 2 * xo + 1) * C + c};
-    f32x4 v[4];
+    const unsigned p = (unsigned)(i / CG);  // output pixel (< 2^31: checked on the host)
+    const unsigned xo = p % (unsigned)wo, t = p / (unsigned)wo;
+    const unsigned yo = t % (unsigned)ho, img = t / (unsigned)ho;
+    const int64_t base = (((int64_t)img * h + 2 * yo) * w + 2 * xo) * C + c;
+    const int64_t off[4] = {base, base + C, base + (int64_t)w * C, base + (int64_t)w * C + C};
+    f32x4 yr[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = bn_relu4(y + off[q], scale, shift, c);
+    for (int q = 0; q < 4; ++q) yr[q] = Vec4<T>::load(y + off[q]);
     int arg[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float best = v[0][e];
+      float best = fmaxf(yr[0][e] * sc[e] + sh[e], 0.0f);
 #pragma unroll
-      for (int q = 1; q < 4; ++q)
-        if (v[q][e] > best) {  // first maximum in row-major window order (ATen, strict >)
-          best = v[q][e];
+      for (int q = 1; q < 4; ++q) {
+        const float v = fmaxf(yr[q][e] * sc[e] + sh[e], 0.0f);
+        if (v > best) {  // first maximum in row-major window order (ATen, strict >)
+          best = v;
           arg[e] = q;
         }
+      }
     }
     const f32x4 g = Vec4<T>::load(dp + i * 4);
 #pragma unroll
@@ -389,8 +417,14 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
       for (int e = 0; e < 4; ++e)
         if (arg[e] == q) o[e] += g[e];
       Vec4<T>::store(dz + off[q], o);
+      if (bn_slab) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = to_f(from_f<T>(o[e]));  // as stored
+        bn.add(yr[q], o, sc, sh, mu, is);
+      }
     }
   }
+  if (bn_slab) channel_block_reduce<3>(bn.acc, C, bn_slab + (int64_t)blockIdx.x * 3 * C);
 }
 
 // =========================================================================== 1x1 heads (C = 64)
@@ -432,7 +466,8 @@ template <typename T>
 __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ w, int nh,
                                  const float* __restrict__ g0, const float* __restrict__ g1,
-                                 const float* __restrict__ g2, T* __restrict__ dz, float* slab) {
+                                 const float* __restrict__ g2, T* __restrict__ dz, float* slab,
+                                 const float* __restrict__ mean, const float* __restrict__ invstd, float* bn_slab) {
   const int sub = threadIdx.x & 15;
   const int c = sub * 4;
   const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
@@ -441,16 +476,28 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
   for (int h = 0; h < 3; ++h) wv[h] = h < nh ? *reinterpret_cast<const f32x4*>(w + h * 64 + c) : f32x4{0, 0, 0, 0};
   f32x4 dw[3] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   float db[3] = {0, 0, 0};
+  f32x4 mu = f32x4{0, 0, 0, 0}, is = f32x4{0, 0, 0, 0};
+  if (bn_slab) {
+    mu = *reinterpret_cast<const f32x4*>(mean + c);
+    is = *reinterpret_cast<const f32x4*>(invstd + c);
+  }
+  BnbAcc bn;
   const int64_t rows = gridDim.x;
   const int64_t chunk = (m + rows - 1) / rows;
   const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(m, p0 + chunk);
   for (int64_t p = p0 + (threadIdx.x >> 4); p < p1; p += (TPB >> 4)) {
-    f32x4 z = Vec4<T>::load(y + p * 64 + c);
+    const f32x4 yv = Vec4<T>::load(y + p * 64 + c);
+    f32x4 z;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[e] = fmaxf(z[e] * sc[e] + sh[e], 0.0f);
+    for (int e = 0; e < 4; ++e) z[e] = fmaxf(yv[e] * sc[e] + sh[e], 0.0f);
     float g[3] = {g0[p], nh > 1 ? g1[p] : 0.0f, nh > 1 ? g2[p] : 0.0f};
     f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];
     Vec4<T>::store(dz + p * 64 + c, d);
+    if (bn_slab) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<T>(d[e]));  // as stored
+      bn.add(yv, d, sc, sh, mu, is);
+    }
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
       dw[h] += z * g[h];
@@ -487,6 +534,7 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     }
     __syncthreads();
   }
+  if (bn_slab) channel_block_reduce<3>(bn.acc, 64, bn_slab + (int64_t)blockIdx.x * 3 * 64);
 }
 
 // =========================================================================== losses
@@ -748,15 +796,28 @@ int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t
   return check_launch("maxpool2_fwd");
 }
 
+int64_t selunet_maxpool2_bwd_slab_rows(int32_t n, int32_t h, int32_t w, int32_t c) {
+  return grid_for((int64_t)n * (h / 2) * (w / 2) * (c / 4), 8192);
+}
+
 int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,
-                         const float* shift, const void* dpool, const void* dskip, void* dz, int32_t dtype,
-                         void* stream) {
-  SELUNET_REQUIRE(y && dpool && dz && scale && shift && n > 0 && h % 2 == 0 && w % 2 == 0 && c % 4 == 0,
+                         const float* shift, const void* dpool, const void* dskip, void* dz,
+                         const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && dpool && dz && scale && shift && n > 0 && h % 2 == 0 && w % 2 == 0 && ok_channels(c),
                   "maxpool2_bwd: bad arguments");
-  const int64_t nv = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(nv, 8192)), dim3(TPB), 0,
-                                       as_stream(stream), (const T*)y, n, h, w, c, scale, shift, (const T*)dpool,
-                                       (const T*)dskip, (T*)dz));
+  SELUNET_REQUIRE((int64_t)n * (h / 2) * (w / 2) < (int64_t(1) << 31), "maxpool2_bwd: grid too large");
+  const float *mean = nullptr, *invstd = nullptr;
+  float* bslab = nullptr;
+  if (bnb && bnb->slab) {
+    SELUNET_REQUIRE(bnb->y == y && bnb->scale == scale && bnb->shift == shift && bnb->mean && bnb->invstd,
+                    "maxpool2_bwd: bnb must describe the pooled layer (same y/scale/shift) with mean/invstd");
+    mean = bnb->mean;
+    invstd = bnb->invstd;
+    bslab = bnb->slab;
+  }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3((unsigned)selunet_maxpool2_bwd_slab_rows(n, h, w, c)),
+                                       dim3(TPB), 0, as_stream(stream), (const T*)y, n, h, w, c, scale, shift,
+                                       (const T*)dpool, (const T*)dskip, (T*)dz, mean, invstd, bslab));
   return check_launch("maxpool2_bwd");
 }
 
@@ -770,14 +831,23 @@ int selunet_heads_fwd(const void* y, int64_t m, const float* scale, const float*
 }
 
 int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float* shift, const float* w, int32_t nh,
-                      const float* g0, const float* g1, const float* g2, void* dz, float* slab, int32_t dtype,
-                      void* stream) {
+                      const float* g0, const float* g1, const float* g2, void* dz, float* slab,
+                      const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(y && scale && shift && w && g0 && dz && slab && m > 0 && (nh == 1 || nh == 3),
                   "heads_bwd: bad arguments");
   SELUNET_REQUIRE(nh == 1 || (g1 && g2), "heads_bwd: g1/g2 required for 3 heads");
+  const float *mean = nullptr, *invstd = nullptr;
+  float* bslab = nullptr;
+  if (bnb && bnb->slab) {
+    SELUNET_REQUIRE(bnb->y == y && bnb->scale == scale && bnb->shift == shift && bnb->mean && bnb->invstd,
+                    "heads_bwd: bnb must describe the heads' input layer (same y/scale/shift) with mean/invstd");
+    mean = bnb->mean;
+    invstd = bnb->invstd;
+    bslab = bnb->slab;
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(heads_bwd_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
                                        as_stream(stream), (const T*)y, m, scale, shift, w, nh, g0, g1, g2, (T*)dz,
-                                       slab));
+                                       slab, mean, invstd, bslab));
   return check_launch("heads_bwd");
 }
 

@@ -45,6 +45,20 @@ class BNState:
 
 
 @dataclass
+class DGrad:
+    """A data gradient plus the per-workgroup partial sums its producing kernel wrote alongside:
+    BN-backward sums [rows][3][C] for a CBR block's dA, or column sums [rows][C] for the up-sampled
+    half of a torch.cat gradient (the ConvTranspose2d bias gradient)."""
+    t: torch.Tensor
+    slab: torch.Tensor = None
+    rows: int = 0
+
+
+def bnb_for(st: BNState, slab) -> K.BnBwdStats:
+    return K.BnBwdStats(K.ptr(st.y), K.ptr(st.scale), K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(slab))
+
+
+@dataclass
 class Ctx:
     dt: torch.dtype
     training: bool
@@ -186,23 +200,23 @@ class Engine:
         return tuple(outs), ctx
 
     # ------------------------------------------------------------------ backward pieces
-    def _cbr_bwd(self, ctx, name, dz, G, input_srcs, dgrad_split=None, need_dgrad=True, q_taps=9, ci_real=None):
-        """BN+ReLU backward then conv weight/bias grads; returns the data gradient (or split pair)."""
+    def _cbr_bwd(self, ctx, name, dg: DGrad, G, input_srcs, dgrad_split=None, need_dgrad=True, q_taps=9,
+                 ci_real=None, prev: BNState = None):
+        """BN+ReLU backward then conv weight/bias grads and the data gradient. dg carries dA and the
+        BN-backward sums its producer wrote. The data gradient comes back as a DGrad whose sums are
+        those of `prev` (the CBR block that produced this layer's input), or a (d(up), d(skip))
+        pair for a concatenated input (d(up) with its column sums)."""
         st: BNState = ctx.bn[name]
         M, co, dev = st.n * st.h * st.w, st.c, st.y.device
-        rows = K.query("selunet_channel_slab_rows", M)
-        slab = torch.empty(rows, 3, co, dtype=torch.float32, device=dev)
-        K.call("selunet_bn_bwd_reduce", K.ptr(dz), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
-               K.ptr(st.mean), K.ptr(st.invstd), K.ptr(slab), self.code, self.stream)
         sums = torch.empty(3 * co, dtype=torch.float64, device=dev)
-        self._reduce(slab, rows, 3 * co, out64=sums)
+        self._reduce(dg.slab, dg.rows, 3 * co, out64=sums)
         coef = torch.empty(3, co, dtype=torch.float32, device=dev)
         gamma = ctx.params[f"{name}.1.weight"]
         K.call("selunet_bn_bwd_finalize", K.ptr(sums), M, co, K.ptr(gamma), K.ptr(st.invstd),
                K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]), K.ptr(coef),
                self.stream)
         dy = torch.empty(M, co, dtype=self.dt, device=dev)
-        K.call("selunet_bn_bwd_apply", K.ptr(dz), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+        K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
         ci = sum(s.channels for s in input_srcs)
@@ -217,46 +231,55 @@ class Engine:
             return None
         _, wd, _ = ctx.wpack[name]
         ga = K.gather(st.n, st.h, st.w, 9, K.source(dy, co))
+        rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
         if dgrad_split is None:
             dx = torch.empty(M, ci, dtype=self.dt, device=dev)
             ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+            slab = None
+            if prev is not None:
+                slab = torch.empty(rows, 3, ci, dtype=torch.float32, device=dev)
+                ep.bnb = bnb_for(prev, slab)
             K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
-            return dx
+            return DGrad(dx, slab, rows)
         c0 = dgrad_split
         d0 = torch.empty(M, c0, dtype=self.dt, device=dev)
         d1 = torch.empty(M, ci - c0, dtype=self.dt, device=dev)
-        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0)
+        colsum = torch.empty(rows, c0, dtype=torch.float32, device=dev)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0, K.ptr(colsum))
         K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
-        return d0, d1
+        return DGrad(d0, colsum, rows), d1
 
-    def _up_bwd(self, ctx, name, du, G, prev: BNState):
-        """ConvTranspose2d(k2,s2) backward: bias/weight grads and the data gradient."""
+    def _up_bwd(self, ctx, name, du: DGrad, G, prev: BNState):
+        """ConvTranspose2d(k2,s2) backward: bias (from du's column sums), weight and data gradients;
+        the data gradient carries prev's BN-backward sums."""
         fwd, wd, ci = ctx.wpack[name]
         co = fwd.shape[0] // 4
         n, h, w = prev.n, prev.h, prev.w
-        dev = du.device
-        Mu = n * 4 * h * w
-        rows = K.query("selunet_channel_slab_rows", Mu)
-        slab = torch.empty(rows, co, dtype=torch.float32, device=dev)
-        K.call("selunet_channel_sum", K.ptr(du), Mu, co, K.ptr(slab), self.code, self.stream)
-        self._reduce(slab, rows, co, out32=G[f"{name}.bias"])
+        dev = du.t.device
+        self._reduce(du.slab, du.rows, co, out32=G[f"{name}.bias"])
         ld = K.query("selunet_wgrad_ld", 4 * co)
         packed = torch.zeros(ci, ld, dtype=torch.float32, device=dev)
         gp = K.gather(n, h, w, 1, prev.src())
-        gq = K.gather(n, h, w, 4, K.source(du, co))
+        gq = K.gather(n, h, w, 4, K.source(du.t, co))
         K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
         K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
         dz = torch.empty(n * h * w, ci, dtype=self.dt, device=dev)
+        ga = K.gather(n, h, w, 4, K.source(du.t, co))
+        rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
+        slab = torch.empty(rows, 3, ci, dtype=torch.float32, device=dev)
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
-        K.call("selunet_gemm_gather", K.gather(n, h, w, 4, K.source(du, co)), K.ptr(wd), ci, 4 * co, ep, self.code,
-               self.stream)
-        return dz
+        ep.bnb = bnb_for(prev, slab)
+        K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
+        return DGrad(dz, slab, rows)
 
-    def _pool_bwd(self, st: BNState, dp, dskip):
+    def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
         dz = torch.empty_like(st.y)
+        rows = K.query("selunet_maxpool2_bwd_slab_rows", st.n, st.h, st.w, st.c)
+        slab = torch.empty(rows, 3, st.c, dtype=torch.float32, device=dz.device)
+        bnb = bnb_for(st, slab)
         K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
-               K.ptr(dp), K.ptr(dskip), K.ptr(dz), self.code, self.stream)
-        return dz
+               K.ptr(dp.t), K.ptr(dskip), K.ptr(dz), bnb, self.code, self.stream)
+        return DGrad(dz, slab, rows)
 
     def backward(self, ctx, P, G, g_heads):
         """g_heads: list of fp32 [N,H,W] grads of (out[, select, aux]) (None -> zeros).
@@ -274,8 +297,11 @@ class Engine:
         rows = K.query("selunet_channel_slab_rows", M)
         nh = len(heads)
         slab = torch.empty(rows, nh * 65, dtype=torch.float32, device=dev)
+        bslab = torch.empty(rows, 3, 64, dtype=torch.float32, device=dev)
         K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
-               K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), self.code, self.stream)
+               K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
+               self.stream)
+        dz = DGrad(dz, bslab, rows)
         hsum = torch.empty(nh, 65, dtype=torch.float32, device=dev)
         self._reduce(slab, rows, nh * 65, out32=hsum)
         for i, h in enumerate(heads):
@@ -287,23 +313,23 @@ class Engine:
         p1, p2, p3 = ctx.pools["pool1"], ctx.pools["pool2"], ctx.pools["pool3"]
         cb = lambda name, d, srcs, **kw: self._cbr_bwd(ctx, name, d, G, srcs, **kw)  # noqa: E731
 
-        dz = cb("decoder_layer_1_1", dz, [bn["decoder_layer_1_2"].src()])
+        dz = cb("decoder_layer_1_1", dz, [bn["decoder_layer_1_2"].src()], prev=bn["decoder_layer_1_2"])
         du1, dskip1 = cb("decoder_layer_1_2", dz, [K.source(u1, 64), e12.src()], dgrad_split=64)
         dz = self._up_bwd(ctx, "unpool1", du1, G, bn["decoder_layer_2_1"])
-        dz = cb("decoder_layer_2_1", dz, [bn["decoder_layer_2_2"].src()])
+        dz = cb("decoder_layer_2_1", dz, [bn["decoder_layer_2_2"].src()], prev=bn["decoder_layer_2_2"])
         du2, dskip2 = cb("decoder_layer_2_2", dz, [K.source(u2, 128), e22.src()], dgrad_split=128)
         dz = self._up_bwd(ctx, "unpool2", du2, G, bn["decoder_layer_3_1"])
-        dz = cb("decoder_layer_3_1", dz, [bn["decoder_layer_3_2"].src()])
+        dz = cb("decoder_layer_3_1", dz, [bn["decoder_layer_3_2"].src()], prev=bn["decoder_layer_3_2"])
         du3, dskip3 = cb("decoder_layer_3_2", dz, [K.source(u3, 256), e32.src()], dgrad_split=256)
         dz = self._up_bwd(ctx, "unpool3", du3, G, bn["decoder_layer_4_1"])
-        dz = cb("decoder_layer_4_1", dz, [bn["decoder_layer_4_2"].src()])
+        dz = cb("decoder_layer_4_1", dz, [bn["decoder_layer_4_2"].src()], prev=bn["decoder_layer_4_2"])
         dp3 = cb("decoder_layer_4_2", dz, [K.source(p3, 256)])
         dz = self._pool_bwd(e32, dp3, dskip3)
-        dz = cb("encoder_layer_3_2", dz, [bn["encoder_layer_3_1"].src()])
+        dz = cb("encoder_layer_3_2", dz, [bn["encoder_layer_3_1"].src()], prev=bn["encoder_layer_3_1"])
         dp2 = cb("encoder_layer_3_1", dz, [K.source(p2, 128)])
         dz = self._pool_bwd(e22, dp2, dskip2)
-        dz = cb("encoder_layer_2_2", dz, [bn["encoder_layer_2_1"].src()])
+        dz = cb("encoder_layer_2_2", dz, [bn["encoder_layer_2_1"].src()], prev=bn["encoder_layer_2_1"])
         dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64)])
         dz = self._pool_bwd(e12, dp1, dskip1)
-        dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()])
+        dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()], prev=bn["encoder_layer_1_1"])
         cb("encoder_layer_1_1", dz, [K.source(ctx.cols, ctx.cols.shape[1])], need_dgrad=False, q_taps=1, ci_real=cin)

@@ -45,7 +45,8 @@ def test_header_declarations_are_exported_and_bound(lib):
 STRUCTS = {
     "selunet_source": (K.Source, ["data", "scale", "shift", "channels", "relu", "layout", "reserved"]),
     "selunet_gather": (K.Gather, ["n", "h", "w", "taps", "nsrc", "reserved", "src"]),
-    "selunet_epilogue": (K.Epilogue, ["out0", "out1", "bias", "stats", "mode", "split"]),
+    "selunet_epilogue": (K.Epilogue, ["out0", "out1", "bias", "stats", "mode", "split", "colsum", "bnb"]),
+    "selunet_bn_bwd_stats": (K.BnBwdStats, ["y", "scale", "shift", "mean", "invstd", "slab"]),
     "selunet_adam_tensor": (K.AdamTensor, ["param", "grad", "exp_avg", "exp_avg_sq", "numel", "chunk_begin"]),
 }
 

@@ -124,17 +124,28 @@ def test_conv3x3_dgrad(cin, cout, split, h, w):
     dyd = nhwc(dy).to(DEV)
     M = n * h * w
     g = K.gather(n, h, w, 9, K.source(dyd, cout))
+    rows = K.query("selunet_gemm_stats_rows", g, cin, K.F32)
     if split:
         d0 = torch.empty(M, split, device=DEV)
         d1 = torch.empty(M, cin - split, device=DEV)
-        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split)
+        colsum = torch.empty(rows, split, device=DEV)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split, K.ptr(colsum))
         K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.F32, K.stream_ptr())
         got = torch.cat((nchw(d0.cpu(), n, h, w), nchw(d1.cpu(), n, h, w)), 1)
+        # column sums of the up-sampled half (the ConvTranspose2d bias gradient)
+        assert rel(colsum.double().sum(0).cpu(), d0.double().sum(0).cpu()) < 1e-6
     else:
         dx = torch.empty(M, cin, device=DEV)
+        # with the fused BatchNorm-backward sums of the producing layer (y, folded BN, batch stats)
+        yprev = gen(M, cin, seed=42).to(DEV)
+        sc, sh = (gen(cin, seed=43).abs() + 0.5).to(DEV), (gen(cin, seed=44) * 0.3).to(DEV)
+        mean, invstd = (gen(cin, seed=45) * 0.1).to(DEV), (gen(cin, seed=46).abs() + 0.5).to(DEV)
+        slab = torch.empty(rows, 3, cin, device=DEV)
         ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+        ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
         K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.F32, K.stream_ptr())
         got = nchw(dx.cpu(), n, h, w)
+        check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
     assert rel(got, ref) < TOL
 
 
@@ -240,8 +251,29 @@ def test_maxpool_ties_and_backward():
     dpd, dsd = d(nhwc(dp)), d(nhwc(dskip))
     dz = torch.empty_like(yd)
     K.call("selunet_maxpool2_bwd", K.ptr(yd), n, h, w, c, K.ptr(sd), K.ptr(td), K.ptr(dpd), K.ptr(dsd), K.ptr(dz),
-           K.F32, K.stream_ptr())
+           None, K.F32, K.stream_ptr())
     assert torch.equal(nchw(dz.cpu(), n, h, w), gz)
+    # fused BatchNorm-backward sums of dz (selunet_bn_bwd_stats)
+    mean, invstd = d(gen(c, seed=40) * 0.1), d(gen(c, seed=41).abs() + 0.5)
+    rows = K.query("selunet_maxpool2_bwd_slab_rows", n, h, w, c)
+    slab = torch.zeros(rows, 3, c, device=DEV)
+    bnb = K.BnBwdStats(K.ptr(yd), K.ptr(sd), K.ptr(td), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+    K.call("selunet_maxpool2_bwd", K.ptr(yd), n, h, w, c, K.ptr(sd), K.ptr(td), K.ptr(dpd), K.ptr(dsd), K.ptr(dz),
+           bnb, K.F32, K.stream_ptr())
+    assert torch.equal(nchw(dz.cpu(), n, h, w), gz)
+    check_bnb_sums(slab, dz, yd, sd, td, mean, invstd)
+
+
+def check_bnb_sums(slab, da, y, scale, shift, mean, invstd, tol=1e-5):
+    """slab [rows][3][C] against (sum da, sum da*xhat, sum xhat), da = dA*[y*scale+shift > 0]."""
+    y64, da64 = y.double(), da.double()
+    m = (y64 * scale.double() + shift.double() > 0).double()
+    g = da64 * m
+    xh = (y64 - mean.double()) * invstd.double()
+    want = torch.stack([g.sum(0), (g * xh).sum(0), xh.sum(0)])
+    got = slab.double().sum(0)
+    scale_ = want.abs().max(dim=1, keepdim=True).values + 1.0
+    assert float(((got - want).abs() / scale_).max()) < tol
 
 
 def test_bn_forward_backward_against_torch():
