@@ -180,6 +180,19 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
  * for columns >= 9c. The first conv then runs as selunet_gemm_gather with taps = 1. */
 int selunet_im2col3x3(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, int32_t k_pad, void* out,
                       int32_t dtype, void* stream);
+/* encoder_layer_1_1's conv (model.py:29) straight from the NCHW fp32 input x [n][cin][h][w]
+ * (cin <= 3) to y [n*h*w][64] in dtype, no bias (it cancels in training-mode BN), with the BN
+ * column statistics of selunet_gemm_gather (stats [selunet_first_conv_rows][2][64], nullable).
+ * wpack: the conv weight from selunet_pack_conv3x3 with k_pad = 32. */
+int64_t selunet_first_conv_rows(int32_t n, int32_t h, int32_t w);
+int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* wpack,
+                           void* y, float* stats, int32_t dtype, void* stream);
+/* Its weight gradient: slab [selunet_first_conv_wgrad_rows][64][32] of per-workgroup partial sums
+ * of dY^T im2col(x) (column k = tap*cin + c); reduce the rows (selunet_reduce_rows) to the packed
+ * [64][32] gradient, then selunet_unpack_conv3x3_grad(.., ld = 32). */
+int64_t selunet_first_conv_wgrad_rows(int32_t n, int32_t h, int32_t w);
+int selunet_first_conv_wgrad(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
+                             float* slab, int32_t dtype, void* stream);
 
 /* ---- MaxPool2d(2) on relu(bn(y)) (model.py:31,35,39) ---------------------------------- */
 int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,

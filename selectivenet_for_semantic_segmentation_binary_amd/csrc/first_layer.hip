@@ -1,0 +1,320 @@
+// First CBR block's convolution (encoder_layer_1_1, model.py:29: C_in = 3 for RGB, 2 for GH
+// input, model.py:24-27) read straight from the network's NCHW fp32 input.
+//
+// Forward: a 16x16-pixel tile per workgroup; the (18x18) x C_in input halo is staged in LDS and
+// every thread builds its pixel's im2col row (K = 9*C_in <= 27, zero padded to 32) in LDS; one
+// MFMA K-pass against the 64x32 weight tile; the LDS-staged epilogue writes y and the BatchNorm
+// column statistics like every other conv. Replaces an im2col pass through HBM (a 64-column
+// bf16 operand: 1 GB at bs=128) and the GEMM that re-read it.
+//
+// Weight gradient: dW[co][k] = sum_p dY[p][co] * im2col(x)[p][k]. Each workgroup walks a range of
+// pixel tiles; per tile the threads write dY and the im2col rows TRANSPOSED into LDS ([co][pixel],
+// [k][pixel]) so the MFMA's reduction dimension (pixels) is contiguous for both operands. The next
+// tile's dY and input are loaded while the current one is multiplied. Per-workgroup partial sums
+// go to a slab reduced deterministically in fp64 (selunet_reduce_rows).
+#include "gemm_common.h"
+
+namespace selunet {
+
+constexpr int FK = 32;                  // padded K of the first layer (9 * C_in <= 27)
+constexpr int FCO = 64;                 // output channels of encoder_layer_1_1 (model.py:29)
+constexpr int FT = 16;                  // pixel tile edge
+constexpr int FH = FT + 2;              // halo edge
+constexpr int FPIX = FT * FT;           // 256 pixels per tile
+constexpr int FTHREADS = 256;
+
+__device__ __forceinline__ void tile_coords(unsigned t, int tiles_x, int tiles_y, int& img, int& y0, int& x0) {
+  const unsigned r = t / (unsigned)tiles_x;
+  x0 = (int)(t - r * (unsigned)tiles_x) * FT;
+  const unsigned im = r / (unsigned)tiles_y;
+  y0 = (int)(r - im * (unsigned)tiles_y) * FT;
+  img = (int)im;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(FTHREADS, 2)
+first_conv_fwd_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ wp, EpiArg ep,
+                      int tiles_x, int tiles_y, int total_tiles) {
+  constexpr int RB = FK * (int)sizeof(T) + 16;  // LDS row bytes (conflict-free 16-row fragment reads)
+  constexpr int XR = (3 * FH * FH + FTHREADS - 1) / FTHREADS;  // halo values per thread
+  // [ A rows + input halo | epilogue tile (aliases them) ][ weights, staged once ]
+  constexpr int SMEM_MAIN = FPIX * RB + 3 * FH * FH * 4;
+  constexpr int SMEM_EPI = FPIX * (FCO + 4) * 4;
+  constexpr int SMEM_T = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_T + FCO * RB];
+  unsigned char* As = smem;
+  float* Xs = reinterpret_cast<float*>(smem + FPIX * RB);
+  unsigned char* Bs = smem + SMEM_T;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  // persistent: tiles b, b + grid, ... (b XCD-remapped so neighbouring tiles share an L2)
+  const unsigned b0 = xcd_remap(blockIdx.x, gridDim.x);
+
+  // the halo of a tile, loaded unconditionally (clamped) into registers one tile ahead
+  struct Halo {
+    float v[XR];
+  };
+  auto load_halo = [&](int t) __attribute__((always_inline)) {
+    Halo hv;
+    int img, y0, x0;
+    tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < XR; ++r) {
+      const int i = min(r * FTHREADS + tid, cin * FH * FH - 1);
+      const int c = i / (FH * FH), rr = i - c * (FH * FH);
+      const int ys = min(max(y0 - 1 + rr / FH, 0), h - 1), xs = min(max(x0 - 1 + rr % FH, 0), w - 1);
+      hv.v[r] = x[(((int64_t)img * cin + c) * h + ys) * w + xs];
+    }
+    return hv;
+  };
+  constexpr int WV = FK * (int)sizeof(T) / 16;  // 16-B vectors per weight row
+  auto stage_weights = [&]() __attribute__((always_inline)) {
+    for (int i = tid; i < FCO * WV; i += FTHREADS) {
+      const int row = i / WV, v = i - row * WV;
+      *reinterpret_cast<uint4*>(Bs + row * RB + v * 16) =
+          *reinterpret_cast<const uint4*>(wp + row * FK + v * (16 / sizeof(T)));
+    }
+  };
+
+  int t = (int)b0;
+  Halo cur = load_halo(t < total_tiles ? t : 0);
+  stage_weights();
+  for (; t < total_tiles; t += gridDim.x) {
+    int img, y0, x0;
+    tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < XR; ++r) {
+      const int i = r * FTHREADS + tid;
+      if (i < cin * FH * FH) {
+        const int c = i / (FH * FH), rr = i - c * (FH * FH);
+        const int ys = y0 - 1 + rr / FH, xs = x0 - 1 + rr % FH;
+        Xs[i] = ((unsigned)ys < (unsigned)h && (unsigned)xs < (unsigned)w) ? cur.v[r] : 0.0f;
+      }
+    }
+    const int tn = t + (int)gridDim.x;
+    cur = load_halo(tn < total_tiles ? tn : t);  // next tile's input, in flight during this one
+    __syncthreads();
+    {
+      const int py = tid / FT, px = tid % FT;
+      T row[FK];
+#pragma unroll
+      for (int k = 0; k < FK; ++k) {
+        float v = 0.0f;
+        if (k < 9 * cin) {
+          const int tap = k / cin, c = k - tap * cin;
+          v = Xs[(c * FH + py + tap / 3) * FH + px + tap % 3];
+        }
+        row[k] = from_f<T>(v);
+      }
+#pragma unroll
+      for (int v = 0; v < WV; ++v) {
+        uint4 u;
+        __builtin_memcpy(&u, reinterpret_cast<const unsigned char*>(row) + v * 16, 16);
+        *reinterpret_cast<uint4*>(As + tid * RB + v * 16) = u;
+      }
+    }
+    __syncthreads();
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+#pragma unroll
+    for (int q = 0; q < FK * (int)sizeof(T) / 32; ++q) {
+      const int boff = q * 32 + half * 16;
+      uint4 af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = *reinterpret_cast<const uint4*>(As + (wave * 64 + a * 32 + l32) * RB + boff);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = *reinterpret_cast<const uint4*>(Bs + (b * 32 + l32) * RB + boff);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+    }
+    __syncthreads();
+
+    float* tile = reinterpret_cast<float*>(smem);
+    acc_to_lds<2, 2, FCO>(tile, acc, wave * 64, 0, lane);
+    __syncthreads();
+    auto dst = [&](int pix, int c) -> T* {
+      const int y = y0 + pix / FT, xx = x0 + pix % FT;
+      if (y >= h || xx >= w) return nullptr;
+      return reinterpret_cast<T*>(ep.out0) + (((int64_t)img * h + y) * w + xx) * FCO + c;
+    };
+    auto bias_col = [&](int c) { return c; };
+    lds_tile_store<T, FPIX, FCO, FTHREADS>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, t, 0, FCO));
+    __syncthreads();  // the tile LDS is restaged by the next iteration
+  }
+}
+
+// ---------------------------------------------------------------------------------- wgrad
+template <typename T>
+__global__ void __launch_bounds__(FTHREADS, 2)
+first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ dy, float* slab,
+                        int tiles_x, int tiles_y, int total_tiles, int tiles_per_block) {
+  constexpr int PB = FPIX * (int)sizeof(T) + 16;  // transposed row bytes (256 pixels + pad)
+  constexpr int E = 16 / (int)sizeof(T);
+  constexpr int DV = FCO / E;                      // 16-B vectors per dY pixel row
+  __shared__ __attribute__((aligned(16))) unsigned char smem[FCO * PB + FK * PB + 3 * FH * FH * 4];
+  unsigned char* Ds = smem;                        // [64 co][256 px]
+  unsigned char* Cs = smem + FCO * PB;             // [32 k][256 px]
+  float* Xs = reinterpret_cast<float*>(Cs + FK * PB);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int wa = wave & 1, wp = wave >> 1;  // co subtile, pixel half
+  const int tb = blockIdx.x * tiles_per_block;
+  const int te = min(total_tiles, tb + tiles_per_block);
+
+  struct Loaded {
+    uint4 d[DV];
+    float xh[(3 * FH * FH + FTHREADS - 1) / FTHREADS];
+  };
+  auto load = [&](int t) __attribute__((always_inline)) {
+    Loaded L;
+    int img, y0, x0;
+    tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
+    const int y = min(y0 + tid / FT, h - 1), xx = min(x0 + tid % FT, w - 1);
+    const T* src = dy + (((int64_t)img * h + y) * w + xx) * FCO;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) L.d[v] = *reinterpret_cast<const uint4*>(src + v * E);
+#pragma unroll
+    for (int r = 0; r < (3 * FH * FH + FTHREADS - 1) / FTHREADS; ++r) {
+      const int i = min(r * FTHREADS + tid, cin * FH * FH - 1);
+      const int c = i / (FH * FH), rr = i - c * (FH * FH);
+      const int ys = min(max(y0 - 1 + rr / FH, 0), h - 1), xs = min(max(x0 - 1 + rr % FH, 0), w - 1);
+      L.xh[r] = x[(((int64_t)img * cin + c) * h + ys) * w + xs];
+    }
+    return L;
+  };
+  auto stage = [&](const Loaded& L, int t) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < (3 * FH * FH + FTHREADS - 1) / FTHREADS; ++r) {
+      const int i = r * FTHREADS + tid;
+      if (i < cin * FH * FH) {
+        const int c = i / (FH * FH), rr = i - c * (FH * FH);
+        const int ys = y0 - 1 + rr / FH, xs = x0 - 1 + rr % FH;
+        Xs[i] = ((unsigned)ys < (unsigned)h && (unsigned)xs < (unsigned)w) ? L.xh[r] : 0.0f;
+      }
+    }
+    // dY row of pixel tid, transposed (a pixel outside the image contributes nothing)
+    const bool inside = y0 + tid / FT < h && x0 + tid % FT < w;
+    T* dcol = reinterpret_cast<T*>(Ds) + tid;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      T e[E];
+      __builtin_memcpy(e, &L.d[v], 16);
+#pragma unroll
+      for (int j = 0; j < E; ++j) dcol[(v * E + j) * (PB / (int)sizeof(T))] = inside ? e[j] : from_f<T>(0.0f);
+    }
+  };
+  auto build_cols = [&]() __attribute__((always_inline)) {
+    const int py = tid / FT, px = tid % FT;
+    T* ccol = reinterpret_cast<T*>(Cs) + tid;
+#pragma unroll
+    for (int k = 0; k < FK; ++k) {
+      float v = 0.0f;
+      if (k < 9 * cin) {
+        const int tap = k / cin, c = k - tap * cin;
+        v = Xs[(c * FH + py + tap / 3) * FH + px + tap % 3];
+      }
+      ccol[k * (PB / (int)sizeof(T))] = from_f<T>(v);
+    }
+  };
+
+  f32x16 acc = f32x16{};
+  if (tb < te) {
+    Loaded cur = load(tb);
+    for (int t = tb; t < te; ++t) {
+      stage(cur, t);
+      __syncthreads();  // Xs, Ds written
+      build_cols();
+      if (t + 1 < te) cur = load(t + 1);
+      __syncthreads();  // Cs written
+      // out[co][k] += sum over this wave's 128 pixels
+#pragma unroll
+      for (int q = 0; q < 128 * (int)sizeof(T) / 32; ++q) {
+        const int boff = wp * 128 * (int)sizeof(T) + q * 32 + half * 16;
+        const uint4 af = *reinterpret_cast<const uint4*>(Ds + (wa * 32 + l32) * PB + boff);
+        const uint4 bfr = *reinterpret_cast<const uint4*>(Cs + l32 * PB + boff);
+        Mma<T>::run(acc, af, bfr);
+      }
+      __syncthreads();  // before the next tile overwrites Ds / Cs / Xs
+    }
+  }
+  // combine the two pixel halves, write this block's [64][32] partial sums
+  float* red = reinterpret_cast<float*>(smem);  // [2][64][32]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = wa * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+    red[(wp * FCO + co) * FK + l32] = acc[r];
+  }
+  __syncthreads();
+  for (int i = tid; i < FCO * FK; i += FTHREADS) slab[(int64_t)blockIdx.x * FCO * FK + i] = red[i] + red[FCO * FK + i];
+}
+
+static int tiles_of(int n, int h, int w, int& tx, int& ty) {
+  tx = (int)cdiv(w, FT);
+  ty = (int)cdiv(h, FT);
+  return n * tx * ty;
+}
+
+static int wgrad_tiles_per_block(int total) { return (int)std::max<int64_t>(1, cdiv(total, 1024)); }
+
+}  // namespace selunet
+
+using namespace selunet;
+
+extern "C" int64_t selunet_first_conv_rows(int32_t n, int32_t h, int32_t w) {
+  int tx, ty;
+  return tiles_of(n, h, w, tx, ty);
+}
+
+extern "C" int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* wpack,
+                                      void* y, float* stats, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(x && wpack && y && n > 0 && h > 0 && w > 0 && cin >= 1 && cin <= 3, "first_conv_fwd: bad arguments");
+  SELUNET_REQUIRE((int64_t)n * cdiv(h, FT) * cdiv(w, FT) < (int64_t(1) << 31), "first_conv_fwd: grid too large");
+  int tx, ty;
+  const int tiles = tiles_of(n, h, w, tx, ty);
+  EpiArg ep{y, nullptr, nullptr, stats, SELUNET_EP_PLAIN, 0, nullptr, BnBwdArg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}};
+  const unsigned blocks = (unsigned)std::min(tiles, 2048);  // 8 tiles in flight per CU pair of workgroups
+  if (dtype == SELUNET_F32)
+    hipLaunchKernelGGL(first_conv_fwd_kernel<float>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h, w,
+                       reinterpret_cast<const float*>(wpack), ep, tx, ty, tiles);
+  else if (dtype == SELUNET_BF16)
+    hipLaunchKernelGGL(first_conv_fwd_kernel<__bf16>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h, w,
+                       reinterpret_cast<const __bf16*>(wpack), ep, tx, ty, tiles);
+  else
+    return fail(SELUNET_EINVAL, "first_conv_fwd: bad dtype %d", dtype);
+  return check_launch("first_conv_fwd");
+}
+
+extern "C" int64_t selunet_first_conv_wgrad_rows(int32_t n, int32_t h, int32_t w) {
+  int tx, ty;
+  const int total = tiles_of(n, h, w, tx, ty);
+  return cdiv(total, wgrad_tiles_per_block(total));
+}
+
+extern "C" int selunet_first_conv_wgrad(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
+                                        float* slab, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(x && dy && slab && n > 0 && h > 0 && w > 0 && cin >= 1 && cin <= 3, "first_conv_wgrad: bad arguments");
+  SELUNET_REQUIRE((int64_t)n * cdiv(h, FT) * cdiv(w, FT) < (int64_t(1) << 31), "first_conv_wgrad: grid too large");
+  int tx, ty;
+  const int total = tiles_of(n, h, w, tx, ty);
+  const int per = wgrad_tiles_per_block(total);
+  const unsigned blocks = (unsigned)cdiv(total, per);
+  if (dtype == SELUNET_F32)
+    hipLaunchKernelGGL(first_conv_wgrad_kernel<float>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h,
+                       w, reinterpret_cast<const float*>(dy), slab, tx, ty, total, per);
+  else if (dtype == SELUNET_BF16)
+    hipLaunchKernelGGL(first_conv_wgrad_kernel<__bf16>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h,
+                       w, reinterpret_cast<const __bf16*>(dy), slab, tx, ty, total, per);
+  else
+    return fail(SELUNET_EINVAL, "first_conv_wgrad: bad dtype %d", dtype);
+  return check_launch("first_conv_wgrad");
+}

@@ -68,13 +68,23 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     rimg[i] = (int)(t / g.h);
   }
 
-  uint4 ra[AR];
-  bool rok[AR];
-  uint4 rb[BR];
-  int st_src = 0, st_c = 0;  // transform selector of the staged slice
+  // One staged K slice, held in registers between its loads and its LDS write. Loads are issued
+  // unconditionally (rows / pixels clamped to valid addresses, zeroed when written to LDS) so the
+  // compiler counts outstanding loads instead of waiting on each; the stage travels by value (a
+  // lambda-captured register array gets demoted to scratch).
+  struct Stage {
+    uint4 a[AR];
+    uint4 b[BR];
+    float scv[E], shv[E];  // folded BN + ReLU coefficients of the staged channels (same for every row)
+    unsigned ok;           // bit i: A row i is inside the image (else zero padding)
+    int src;
+  };
 
   auto load_stage = [&](int kc) __attribute__((always_inline)) {
+    Stage st;
     const int k0 = kc * BKE;
+    st.ok = 0;
+    st.src = 0;
     if constexpr (!SMALL) {
       const int tap = k0 / g.Ctot;
       int c0 = k0 - tap * g.Ctot;
@@ -83,21 +93,27 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
         c0 -= g.src[0].C;
         s = 1;
       }
-      st_src = s;
-      st_c = c0 + cc * E;
+      st.src = s;
+      const int st_c = c0 + cc * E;
       const SrcArg sa = pick_src(g, s);
       const T* base = reinterpret_cast<const T*>(sa.data);
+      // (always loaded — from the weights when there is no transform — so no branch per element)
+      const bool xf = sa.scale != nullptr;
+      const float* scp = xf ? sa.scale + st_c : reinterpret_cast<const float*>(B);
+      const float* shp = xf ? sa.shift + st_c : reinterpret_cast<const float*>(B);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        st.scv[e] = scp[e];
+        st.shv[e] = shp[e];
+      }
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         int ys, xs;
-        const bool ok = rv[i] && src_pixel(g, tap, ry[i], rx[i], ys, xs);
-        rok[i] = ok;
-        if (ok) {
-          const int64_t off = (((int64_t)rimg[i] * g.hs + ys) * g.ws + xs) * sa.C + st_c;
-          ra[i] = *reinterpret_cast<const uint4*>(base + off);
-        } else {
-          ra[i] = make_uint4(0, 0, 0, 0);
-        }
+        if (rv[i] && src_pixel(g, tap, ry[i], rx[i], ys, xs)) st.ok |= 1u << i;
+        ys = min(max(ys, 0), g.hs - 1);
+        xs = min(max(xs, 0), g.ws - 1);
+        const int64_t off = (((int64_t)rimg[i] * g.hs + ys) * g.ws + xs) * sa.C + st_c;
+        st.a[i] = *reinterpret_cast<const uint4*>(base + off);
       }
     } else {
 #pragma unroll
@@ -106,39 +122,33 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
         const int64_t m = m0 + rr + 32 * i;
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = from_f<T>(gather_scalar<T>(g, m, k0 + cc * E + e));
-        __builtin_memcpy(&ra[i], v, 16);
-        rok[i] = true;
+        __builtin_memcpy(&st.a[i], v, 16);
+        st.ok |= 1u << i;
       }
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int n = n0 + rr + 32 * i;
-      rb[i] = *reinterpret_cast<const uint4*>(B + (int64_t)n * k_pad + k0 + cc * E);
+      st.b[i] = *reinterpret_cast<const uint4*>(B + (int64_t)n * k_pad + k0 + cc * E);
     }
+    return st;
   };
 
-  auto store_stage = [&](int buf) __attribute__((always_inline)) {
+  auto store_stage = [&](const Stage& st, int buf) __attribute__((always_inline)) {
     unsigned char* a_dst = As + buf * BM * ROWB;
     unsigned char* b_dst = Bs + buf * BN * ROWB;
-    const SrcArg sa = pick_src(g, st_src);
+    const SrcArg sa = pick_src(g, st.src);
     if (!SMALL && sa.scale != nullptr) {
-      // folded BN + ReLU of the producer; the 8 (bf16) / 4 (fp32) channel coefficients are the
-      // same for every row this thread stages
-      float scv[E], shv[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        scv[e] = sa.scale[st_c + e];
-        shv[e] = sa.shift[st_c + e];
-      }
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         T v[E];
-        __builtin_memcpy(v, &ra[i], 16);
+        __builtin_memcpy(v, &st.a[i], 16);
+        const bool ok = (st.ok >> i) & 1u;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          float f = to_f(v[e]) * scv[e] + shv[e];
+          float f = to_f(v[e]) * st.scv[e] + st.shv[e];
           f = sa.relu ? fmaxf(f, 0.0f) : f;
-          v[e] = from_f<T>(rok[i] ? f : 0.0f);
+          v[e] = from_f<T>(ok ? f : 0.0f);
         }
         uint4 o;
         __builtin_memcpy(&o, v, 16);
@@ -146,11 +156,13 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = ra[i];
+      for (int i = 0; i < AR; ++i)
+        *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) =
+            ((st.ok >> i) & 1u) ? st.a[i] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(b_dst + (rr + 32 * i) * ROWB + cc * 16) = rb[i];
+      *reinterpret_cast<uint4*>(b_dst + (rr + 32 * i) * ROWB + cc * 16) = st.b[i];
   };
 
   f32x16 acc[MT][NT];
@@ -160,13 +172,13 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
 
   const int nk = k_pad / BKE;
-  load_stage(0);
-  store_stage(0);
+  {
+    const Stage st0 = load_stage(0);
+    store_stage(st0, 0);
+  }
   __syncthreads();
 
-  for (int kc = 0; kc < nk; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < nk) load_stage(kc + 1);
+  auto mma_stage = [&](int buf) __attribute__((always_inline)) {
     const unsigned char* a_src = As + buf * BM * ROWB;
     const unsigned char* b_src = Bs + buf * BN * ROWB;
 #pragma unroll
@@ -184,9 +196,16 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 #pragma unroll
         for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
     }
-    if (kc + 1 < nk) store_stage(buf ^ 1);
+  };
+  for (int kc = 0; kc + 1 < nk; ++kc) {
+    const Stage nxt = load_stage(kc + 1);
+    __builtin_amdgcn_sched_barrier(0);  // all of the next stage's loads ahead of this stage's MFMAs
+    mma_stage(kc & 1);
+    store_stage(nxt, (kc & 1) ^ 1);
     __syncthreads();
   }
+  mma_stage((nk - 1) & 1);
+  __syncthreads();
 
   // ------------------------------------------------------------------ epilogue (LDS-staged)
   float* tile = reinterpret_cast<float*>(smem);  // [BM][BN + 4]; the loop ended with a barrier
@@ -202,12 +221,10 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
                             : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
     const int ab = col / Cq, cq = col - ab * Cq;
-    const int x = (int)(m % g.w);
-    const int64_t t = m / g.w;
-    const int y = (int)(t % g.h);
-    const int64_t img = t / g.h;
+    const unsigned mu = (unsigned)m, x = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
+    const unsigned y = t % (unsigned)g.h, img = t / (unsigned)g.h;
     return reinterpret_cast<T*>(ep.out0) +
-           ((img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + cq;
+           (((int64_t)img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + cq;
   };
   auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
   lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, m_tile, n0, N));

@@ -260,10 +260,10 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
     a[e] = k2i;
     b[e] = coef[C + c + e] - k2i * mean[c + e];
   }
-  for (int64_t p = blockIdx.x * (int64_t)PL + pl; p < m; p += (int64_t)gridDim.x * PL) {
-    const int64_t off = p * C + c;
-    const f32x4 y0 = Vec4<T>::load(y + off), y1 = Vec4<T>::load(y + off + 4);
-    const f32x4 g0 = Vec4<T>::load(dz + off), g1 = Vec4<T>::load(dz + off + 4);
+  // U pixels per thread and iteration, all loads issued before any use (loads in flight per wave)
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * PL;
+  auto one = [&](const f32x4& y0, const f32x4& y1, const f32x4& g0, const f32x4& g1, int64_t off) {
     f32x4 o0, o1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -272,6 +272,25 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
     }
     Vec4<T>::store(dy + off, o0);
     Vec4<T>::store(dy + off + 4, o1);
+  };
+  int64_t p = blockIdx.x * (int64_t)PL + pl;
+  for (; p + (U - 1) * stride < m; p += U * stride) {
+    f32x4 y0[U], y1[U], g0[U], g1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (p + u * stride) * C + c;
+      y0[u] = Vec4<T>::load(y + off);
+      y1[u] = Vec4<T>::load(y + off + 4);
+      g0[u] = Vec4<T>::load(dz + off);
+      g1[u] = Vec4<T>::load(dz + off + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(y0[u], y1[u], g0[u], g1[u], (p + u * stride) * C + c);
+  }
+  for (; p < m; p += stride) {
+    const int64_t off = p * C + c;
+    one(Vec4<T>::load(y + off), Vec4<T>::load(y + off + 4), Vec4<T>::load(dz + off), Vec4<T>::load(dz + off + 4),
+        off);
   }
 }
 

@@ -22,6 +22,7 @@ from . import layout as LY
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+FIRST_KPAD = 32  # packed K of encoder_layer_1_1 (9 * C_in <= 27), see selunet_first_conv_fwd
 
 
 def _rup(a, b):
@@ -95,7 +96,7 @@ class Engine:
         for name, ci, co in LY.CBR_LAYERS:
             w = P[f"{name}.0.weight"]
             ci = w.shape[1]
-            kpad = _rup(9 * ci, self.bke)
+            kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
             fwd = torch.empty(co, kpad, dtype=self.dt, device=dev)
             dg = None
             if need_dgrad and name != "encoder_layer_1_1":
@@ -111,19 +112,28 @@ class Engine:
         return packs
 
     # ------------------------------------------------------------------ forward pieces
-    def _cbr(self, ctx, name, P, B, n, h, w, *srcs, taps=9):
+    def _cbr(self, ctx, name, P, B, n, h, w, *srcs, taps=9, first_x=None):
+        """CBR_2D forward (model.py:9-15): conv (+ BN batch statistics in its epilogue), BN finalize.
+        first_x: the network input (NCHW fp32) for encoder_layer_1_1, convolved directly."""
         fwd, _, kpad = ctx.wpack[name]
         co = fwd.shape[0]
         M = n * h * w
         dev = fwd.device
         y = torch.empty(M, co, dtype=self.dt, device=dev)
         stats = None
-        g = K.gather(n, h, w, taps, *srcs)
-        rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
+        if first_x is not None:
+            rows = K.query("selunet_first_conv_rows", n, h, w)
+        else:
+            g = K.gather(n, h, w, taps, *srcs)
+            rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
         if ctx.training:
             stats = torch.empty(rows, 2, co, dtype=torch.float32, device=dev)
-        ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
-        K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
+        if first_x is not None:
+            K.call("selunet_first_conv_fwd", K.ptr(first_x), n, first_x.shape[1], h, w, K.ptr(fwd), K.ptr(y),
+                   K.ptr(stats), self.code, self.stream)
+        else:
+            ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+            K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
         mean, invstd, scale, shift = (torch.empty(co, dtype=torch.float32, device=dev) for _ in range(4))
         sums = None
         if ctx.training:
@@ -164,11 +174,8 @@ class Engine:
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
         h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
-        # first layer (C_in = 3): explicit im2col, then a dense GEMM (taps = 1)
-        kpad0 = ctx.wpack["encoder_layer_1_1"][2]
-        ctx.cols = torch.empty(n * H * W, kpad0, dtype=self.dt, device=x.device)
-        K.call("selunet_im2col3x3", K.ptr(x), n, cin, H, W, kpad0, K.ptr(ctx.cols), self.code, self.stream)
-        e11 = self._cbr(ctx, "encoder_layer_1_1", P, B, n, h1, w1, K.source(ctx.cols, kpad0), taps=1)
+        # first layer (C_in = 3 or 2): convolved straight from the NCHW fp32 input
+        e11 = self._cbr(ctx, "encoder_layer_1_1", P, B, n, h1, w1, first_x=x)
         e12 = c("encoder_layer_1_2", h1, w1, e11.src())
         p1 = self._pool(ctx, "pool1", e12)
         e21 = c("encoder_layer_2_1", h2, w2, K.source(p1, 64))
@@ -201,7 +208,7 @@ class Engine:
 
     # ------------------------------------------------------------------ backward pieces
     def _cbr_bwd(self, ctx, name, dg: DGrad, G, input_srcs, dgrad_split=None, need_dgrad=True, q_taps=9,
-                 ci_real=None, prev: BNState = None):
+                 prev: BNState = None, first_x=None):
         """BN+ReLU backward then conv weight/bias grads and the data gradient. dg carries dA and the
         BN-backward sums its producer wrote. The data gradient comes back as a DGrad whose sums are
         those of `prev` (the CBR block that produced this layer's input), or a (d(up), d(skip))
@@ -219,14 +226,24 @@ class Engine:
         K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
+        if first_x is not None:
+            cin = first_x.shape[1]
+            rows = K.query("selunet_first_conv_wgrad_rows", st.n, st.h, st.w)
+            slab = torch.empty(rows, co, FIRST_KPAD, dtype=torch.float32, device=dev)
+            K.call("selunet_first_conv_wgrad", K.ptr(first_x), st.n, cin, st.h, st.w, K.ptr(dy), K.ptr(slab),
+                   self.code, self.stream)
+            packed = torch.empty(co, FIRST_KPAD, dtype=torch.float32, device=dev)
+            self._reduce(slab, rows, co * FIRST_KPAD, out32=packed)
+            K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, cin, FIRST_KPAD, K.ptr(G[f"{name}.0.weight"]),
+                   self.stream)
+            return None
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
         packed = torch.zeros(co, ld, dtype=torch.float32, device=dev)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
         K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
-        ci_w = ci if ci_real is None else ci_real  # im2col operand: packed columns are (tap, ci) already
-        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci_w, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
+        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
         if not need_dgrad:
             return None
         _, wd, _ = ctx.wpack[name]
@@ -332,4 +349,4 @@ class Engine:
         dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64)])
         dz = self._pool_bwd(e12, dp1, dskip1)
         dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()], prev=bn["encoder_layer_1_1"])
-        cb("encoder_layer_1_1", dz, [K.source(ctx.cols, ctx.cols.shape[1])], need_dgrad=False, q_taps=1, ci_real=cin)
+        cb("encoder_layer_1_1", dz, [], need_dgrad=False, first_x=ctx.x)

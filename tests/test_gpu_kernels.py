@@ -400,3 +400,40 @@ def test_convT_bf16_wgrad():
     gwd = torch.empty(cin, cout, 2, 2, device=DEV)
     K.call("selunet_unpack_convT_grad", K.ptr(packed), cin, cout, K.ptr(gwd), K.stream_ptr())
     assert rel(gwd.cpu(), gw) < 1e-3
+
+
+@pytest.mark.parametrize("dt,cin,n,h,w", [(torch.float32, 3, 2, 32, 32), (torch.float32, 2, 1, 20, 40),
+                                          (torch.bfloat16, 3, 2, 32, 48), (torch.bfloat16, 3, 3, 64, 64)])
+def test_first_conv_fwd_and_wgrad(dt, cin, n, h, w):
+    """encoder_layer_1_1 (model.py:29) straight from the NCHW fp32 input: forward with BN column
+    statistics, and the weight gradient through the row slab."""
+    x = gen(n, cin, h, w, seed=50)
+    wt = gen(64, cin, 3, 3, seed=51, scale=0.2)
+    ref = F.conv2d(x, wt, padding=1)
+    tol = TOL if dt == torch.float32 else 1e-2
+    xd, wd = x.to(DEV).contiguous(), wt.to(DEV).contiguous()
+    fwd = torch.empty(64, 32, dtype=dt, device=DEV)
+    K.call("selunet_pack_conv3x3", K.ptr(wd), 64, cin, 32, K.ptr(fwd), None, K.dtype_code(dt), K.stream_ptr())
+    M = n * h * w
+    y = torch.empty(M, 64, dtype=dt, device=DEV)
+    rows = K.query("selunet_first_conv_rows", n, h, w)
+    stats = torch.empty(rows, 2, 64, device=DEV)
+    K.call("selunet_first_conv_fwd", K.ptr(xd), n, cin, h, w, K.ptr(fwd), K.ptr(y), K.ptr(stats), K.dtype_code(dt),
+           K.stream_ptr())
+    assert rel(nchw(y.float().cpu(), n, h, w), ref) < tol
+    r64 = ref.double().permute(1, 0, 2, 3).reshape(64, -1)
+    st = stats.double().sum(0).cpu()
+    assert rel(st[0], r64.sum(1)) < tol and rel(st[1], (r64 * r64).sum(1)) < tol
+    # weight gradient
+    dy = gen(n, 64, h, w, seed=52)
+    dyq = dy.to(dt).float()  # what the kernel sees
+    ref_w = torch.nn.grad.conv2d_weight(x, wt.shape, dyq, padding=1)
+    dyd = nhwc(dy).to(dt).to(DEV)
+    wrows = K.query("selunet_first_conv_wgrad_rows", n, h, w)
+    slab = torch.empty(wrows, 64, 32, device=DEV)
+    K.call("selunet_first_conv_wgrad", K.ptr(xd), n, cin, h, w, K.ptr(dyd), K.ptr(slab), K.dtype_code(dt),
+           K.stream_ptr())
+    packed = slab.double().sum(0).float().contiguous()
+    gw = torch.empty(64, cin, 3, 3, device=DEV)
+    K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), 64, cin, 32, K.ptr(gw), K.stream_ptr())
+    assert rel(gw.cpu(), ref_w) < (TOL if dt == torch.float32 else 1e-2)
