@@ -177,6 +177,7 @@ def main():
 
     x, lab = make_batch(args.batch, args.size, seed=0)
     lo, hi = parallel.chunk_bounds(args.batch, rank, world)
+    parallel.set_global_batch(args.batch)
     xt = torch.tensor(x[lo:hi], device=dev)
     lt = torch.tensor(lab[lo:hi], device=dev)
     del x, lab

@@ -255,6 +255,23 @@ int selunet_adam_step(const selunet_adam_tensor* list, int32_t n, int64_t total_
                       float beta1, float beta2, float eps, float weight_decay, int64_t step,
                       void* stream);
 
+/* ---- training-loop I/O ------------------------------------- */
+/* Pre-decoded patches -> network input and BCE target, replacing PatchDataset.__getitem__'s
+ * numpy transforms (utils/data_utils.py:94-125,160-168,220-221; train.py:189-191).
+ * img: uint8 NHWC [n][h][w][cin] (cin = 3, RGB); lab: uint8 [n][h][w] raw mask values (only 255
+ * maps to 1); flips: uint8 [n] (bit 0 = np.fliplr, bit 1 = np.flipud; NULL = none).
+ * x: fp32 NCHW [n][3][h][w] = (float32(v/255.0) - 0.5)/0.5; target: fp32 [n][h][w] in {0,1}. */
+int selunet_prep_batch(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n,
+                       int32_t h, int32_t w, int32_t cin, float* x, float* target, void* stream);
+/* Per-batch metrics of train.py:211-238 / eval.py:218-246 accumulated on the device:
+ * counts[6] (uint64, caller-zeroed, accumulated across calls) = {cm[0][0], cm[0][1], cm[1][0],
+ * cm[1][1], selected, total} with cm[label][pred] = Evaluator.confusion_matrix
+ * (utils/compute_metric.py:10-26) over pixels whose selection logit >= t_sel (all pixels when
+ * sel is NULL); pred = out >= t_out. t_out / t_sel: the smallest fp32 logit the reference's
+ * host rule (sigmoid in fp64 or fp32, then > cut_off) maps to 1. */
+int selunet_seg_metrics(const float* out, const float* sel, const float* target, int64_t p,
+                        float t_out, float t_sel, unsigned long long* counts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -93,6 +93,8 @@ SIGNATURES = {
     "selunet_bce_finalize": (c_int32, [P, c_double, P, P]),
     "selunet_bce_bwd": (c_int32, [P, P, c_int64, c_double, P, P, P]),
     "selunet_adam_step": (c_int32, [P, c_int32, c_int64, c_float, c_float, c_float, c_float, c_float, c_int64, P]),
+    "selunet_prep_batch": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
+    "selunet_seg_metrics": (c_int32, [P, P, P, c_int64, c_float, c_float, P, P]),
 }
 
 _lib = None

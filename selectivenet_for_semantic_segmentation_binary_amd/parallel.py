@@ -23,7 +23,7 @@ import os
 import torch
 import torch.distributed as dist
 
-_STATE = {"enabled": False, "group": None}
+_STATE = {"enabled": False, "group": None, "global_batch": None}
 
 
 def init_data_parallel(backend: str | None = None, group=None) -> tuple[int, int]:
@@ -41,6 +41,17 @@ def init_data_parallel(backend: str | None = None, group=None) -> tuple[int, int
 def disable():
     _STATE["enabled"] = False
     _STATE["group"] = None
+    _STATE["global_batch"] = None
+
+
+def set_global_batch(batch: int | None):
+    """Register the global batch size B the ranks' chunks come from (chunk_bounds), so the losses
+    know the global pixel count B*H*W without an exchange (selective_loss.global_count)."""
+    _STATE["global_batch"] = None if batch is None else int(batch)
+
+
+def global_batch() -> int | None:
+    return _STATE["global_batch"]
 
 
 def is_initialized() -> bool:
@@ -106,5 +117,7 @@ def chunk_bounds(batch: int, rank_: int, world: int) -> tuple[int, int]:
 def local_batch(x: torch.Tensor, rank_: int | None = None, world: int | None = None) -> torch.Tensor:
     r = rank() if rank_ is None else rank_
     w = world_size() if world is None else world
+    if rank_ is None and world is None:
+        set_global_batch(x.shape[0])
     lo, hi = chunk_bounds(x.shape[0], r, w)
     return x[lo:hi]

@@ -43,23 +43,28 @@ def _reduced_sums(slab, rows, cols):
 
 
 def _global_count(p_local: int) -> float:
-    if not parallel.is_initialized():
-        return float(p_local)
     t = torch.tensor([float(p_local)], dtype=torch.float64,
                      device="cuda" if torch.cuda.is_available() else "cpu")
     parallel.allreduce_sums(t)
     return float(t.item())
 
 
-_COUNT_CACHE = {}
+def global_count(shape) -> float:
+    """Global pixel count of the data-parallel batch whose local part has `shape` (N, H, W).
 
-
-def global_count(p_local: int) -> float:
-    """Global pixel count of the data-parallel batch (cached per local size and world)."""
-    key = (p_local, parallel.world_size())
-    if key not in _COUNT_CACHE:
-        _COUNT_CACHE[key] = _global_count(p_local)
-    return _COUNT_CACHE[key]
+    With the global batch registered (parallel.set_global_batch / parallel.local_batch) it is
+    B * H * W with no exchange; otherwise one all-reduce of the local count, every call — never
+    cached, since ranks may hold chunks of different sizes (torch.chunk of a ragged last batch)
+    and a rank answering from a cache while another all-reduces would deadlock."""
+    p_local = 1
+    for d in shape:
+        p_local *= int(d)
+    if not parallel.is_initialized():
+        return float(p_local)
+    b = parallel.global_batch()
+    if b is not None and int(shape[0]) > 0:
+        return float(b * (p_local // int(shape[0])))
+    return _global_count(p_local)
 
 
 class _SelectiveRiskB(torch.autograd.Function):
@@ -72,7 +77,7 @@ class _SelectiveRiskB(torch.autograd.Function):
         K.call("selunet_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), p, K.ptr(slab),
                K.stream_ptr())
         sums = _reduced_sums(slab, rows, 2)
-        p_global = global_count(p)
+        p_global = global_count(output.shape)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         coverage = torch.empty((), dtype=torch.float32, device=dev)
         state = torch.empty(4, dtype=torch.float32, device=dev)
@@ -115,7 +120,7 @@ class _BCEWithLogitsMean(torch.autograd.Function):
         slab = torch.empty(rows, 1, dtype=torch.float32, device=dev)
         K.call("selunet_bce_partials", K.ptr(logit), K.ptr(target), p, K.ptr(slab), K.stream_ptr())
         sums = _reduced_sums(slab, rows, 1)
-        p_global = global_count(p)
+        p_global = global_count(logit.shape)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         K.call("selunet_bce_finalize", K.ptr(sums), p_global, K.ptr(loss), K.stream_ptr())
         ctx.save_for_backward(logit, target)

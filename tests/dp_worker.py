@@ -27,6 +27,7 @@ def main(fname, out):
     assert world == int(d["meta_chunks"]), (world, int(d["meta_chunks"]))
     x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
     lo, hi = parallel.chunk_bounds(n, rank, world)
+    parallel.set_global_batch(n)
     xt = torch.tensor(x[lo:hi], device="cuda")
     lt = torch.tensor(lab[lo:hi], device="cuda")
     net = build(selective, int(d["meta_seed"]))

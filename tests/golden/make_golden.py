@@ -324,7 +324,75 @@ def kats():
     print(f"wrote {path}: bce={bce:.4f} ce={ce:.4f} miou={data['miou']:.6f} thr={train_thr!r},{eval_thr!r}")
 
 
+def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0):
+    """mIoU parity run (BASELINE.json 'mIoU parity'): the reference training loop
+    (train.py:183-241: forward, BCEWithLogits aux + calc_selective_risk_image_b, Adam, the
+    per-batch Evaluator on the fp64-sigmoid masks) for `epochs` passes over a seeded synthetic
+    train set in fixed order (no shuffle, no flips), then an eval-mode pass over a validation set
+    (train.py:274-318). Records per-step losses, the training-phase confusion matrix, and the
+    validation confusion matrices / mIoU (selective and plain Evaluator)."""
+    from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess
+
+    ti, tl = make_patches(n_train, size, seed=2024)
+    vi, vl = make_patches(n_val, size, seed=2025)
+    xtr, ltr = preprocess(ti, tl)
+    xva, lva = preprocess(vi, vl)
+    torch.manual_seed(0)
+    net = build_ref(seed, True)
+    optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+    loss_A = torch.nn.BCEWithLogitsLoss()
+    fn_sigmoid = lambda x: 1 / (1 + np.exp(-x.astype("float64")))  # noqa: E731  train.py:150
+    ev = Evaluator(num_class=2, selective=True)
+    losses, total, reject = [], 0, 0
+    net.train()
+    for ep in range(epochs):
+        for b0 in range(0, n_train, bs):
+            x, lab = torch.tensor(xtr[b0:b0 + bs]), torch.tensor(ltr[b0:b0 + bs])
+            output, selection, aux = net(x)
+            loss = loss_A(aux, lab) + ref_loss.calc_selective_risk_image_b(output, selection, target=lab,
+                                                                             lamb=lamb)[0]
+            optim.zero_grad()
+            loss.backward()
+            optim.step()
+            losses.append(loss.item())
+            with np.errstate(over="ignore"):
+                pred = (1.0 * (fn_sigmoid(output.detach().numpy()) > 0.5)).astype("uint8")
+                sel = 1.0 * (fn_sigmoid(selection.detach().numpy()) > 0.5)
+            total += lab.numel()
+            reject += lab.numel() - int(sel.sum())
+            ev.add_batch(lab.numpy().astype("uint8"), pred, selection=sel)
+    out = {"meta_n_train": n_train, "meta_n_val": n_val, "meta_size": size, "meta_bs": bs, "meta_epochs": epochs,
+           "meta_lamb": lamb, "meta_seed": seed, "meta_train_seed": 2024, "meta_val_seed": 2025,
+           "train_losses": np.array(losses), "train_cm": ev.confusion_matrix.copy(),
+           "train_selected": np.int64(total - reject), "train_total": np.int64(total)}
+    net.eval()
+    evs, evp = Evaluator(num_class=2, selective=True), Evaluator(num_class=2, selective=False)
+    vlosses, vsel = [], 0
+    with torch.no_grad():
+        for b0 in range(0, n_val, bs):
+            x, lab = torch.tensor(xva[b0:b0 + bs]), torch.tensor(lva[b0:b0 + bs])
+            output, selection, aux = net(x)
+            vlosses.append((loss_A(aux, lab) + ref_loss.calc_selective_risk_image_b(output, selection, lab,
+                                                                                      lamb=lamb)[0]).item())
+            with np.errstate(over="ignore"):
+                pred = (1.0 * (fn_sigmoid(output.numpy()) > 0.5)).astype("uint8")
+                sel = 1.0 * (fn_sigmoid(selection.numpy()) > 0.5)
+            vsel += int(sel.sum())
+            evs.add_batch(lab.numpy().astype("uint8"), pred, selection=sel)
+            evp.add_batch(lab.numpy().astype("uint8"), pred)
+    out.update({"val_losses": np.array(vlosses), "val_cm_selective": evs.confusion_matrix.copy(),
+                "val_cm": evp.confusion_matrix.copy(), "val_miou_selective": np.float64(evs.get_mIoU()),
+                "val_miou": np.float64(evp.get_mIoU()), "val_selected": np.int64(vsel)})
+    path = os.path.join(HERE, fname)
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}: train loss {losses[0]:.4f} -> {losses[-1]:.4f}, val mIoU {out['val_miou']:.4f} "
+          f"(selective {out['val_miou_selective']:.4f}), val selected {vsel}/{n_val * size * size}")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["miou"]:
+        miou_fixture()
+        sys.exit(0)
     kats()
     loss_cases()
     step_fixture("step_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
@@ -333,3 +401,4 @@ if __name__ == "__main__":
     step_fixture("dp_sel_n8_32_c4.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=4)
     step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=True)
     eval_fixture("eval_sel_n4_64.npz")
+    miou_fixture()

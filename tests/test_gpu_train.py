@@ -1,0 +1,147 @@
+"""Training-loop pieces on the GPU: batch preparation, on-device metrics, the mIoU parity run
+against the reference's own training loop (tests/golden/miou_sel_64.npz, written by
+tests/golden/make_golden.py from the reference model/loss/Evaluator), and the train.py CLI.
+
+Tolerances: prep and metric counts are integer/byte work -> bit-exact. mIoU: |delta| <= 0.002
+(BASELINE.json north_star) for the fp32 path; the bf16 path is held to 0.01.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import selectivenet_for_semantic_segmentation_binary_amd as S
+from oracle import unet_b_cpu as O
+from selectivenet_for_semantic_segmentation_binary_amd import data as D
+from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics, logit_threshold, mean_iou
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess
+from tests import _golden as G
+from tests.test_gpu_model import build
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_prep_batch_bit_exact():
+    rng = np.random.Generator(np.random.PCG64(5))
+    n, h, w = 5, 24, 36
+    imgs = rng.integers(0, 256, (n, h, w, 3), dtype=np.uint8)
+    labs = rng.choice(np.array([0, 1, 128, 250, 254, 255], np.uint8), size=(n, h, w))
+    flips = np.array([0, 1, 2, 3, 1], np.uint8)
+    x, t = D.prep_batch(torch.tensor(imgs, device=DEV), torch.tensor(labs, device=DEV),
+                        torch.tensor(flips, device=DEV))
+    for i in range(n):
+        im, lb = imgs[i], labs[i]
+        if flips[i] & 1:  # RandomFlip: fliplr first, then flipud (utils/data_utils.py:113-121)
+            im, lb = np.fliplr(im), np.fliplr(lb)
+        if flips[i] & 2:
+            im, lb = np.flipud(im), np.flipud(lb)
+        xe, te = preprocess(np.ascontiguousarray(im)[None], np.ascontiguousarray(lb)[None])
+        assert np.array_equal(x[i].cpu().numpy().view(np.uint32), xe[0].view(np.uint32)), i
+        assert np.array_equal(t[i].cpu().numpy(), te[0]), i
+    assert float(t.max()) == 1.0 and set(np.unique(t.cpu().numpy())) <= {0.0, 1.0}
+
+
+@pytest.mark.parametrize("rule", ["train", "eval"])
+def test_seg_metrics_bit_exact(rule):
+    rng = np.random.Generator(np.random.PCG64(11))
+    p = 4 * 3 * 50 + 3  # ragged tail (not a multiple of 4)
+    thr = np.float32(logit_threshold(rule))
+    out = rng.normal(0, 1e-6, p).astype(np.float32)
+    sel = rng.normal(0, 1e-6, p).astype(np.float32)
+    # values straddling the exact decision boundary, +-inf, nan, saturated
+    edge = np.array([thr, np.nextafter(thr, np.float32(-1)), np.nextafter(thr, np.float32(1)), 0, -0.0, np.inf,
+                     -np.inf, np.nan, 40, -40], np.float32)
+    out[:len(edge)] = edge
+    sel[5:5 + len(edge)] = edge
+    tgt = (rng.random(p) > 0.4).astype(np.float32)
+    mask = O.train_pred_mask if rule == "train" else O.eval_pred_mask
+    with np.errstate(over="ignore", invalid="ignore"):
+        pred, smask = mask(out), mask(sel)
+    for selective in (False, True):
+        m = SegMetrics(DEV, selective=selective, rule=rule)
+        ot, st, tt = (torch.tensor(a, device=DEV) for a in (out, sel, tgt))
+        m.add_batch(ot, tt, st)
+        m.add_batch(ot, tt, st)  # accumulates
+        cm = O.confusion_matrix(tgt.astype("uint8"), pred, selection=smask if selective else None)
+        assert np.array_equal(m.confusion_matrix(), 2 * cm)
+        selected, total = m.selected_total()
+        assert total == 2 * p
+        assert selected == (2 * int(smask.sum()) if selective else 2 * p)
+
+
+def _loop(net, xs, ls, bs, epochs, lamb, training, metrics):
+    loss_A = S.BCEWithLogitsLoss()
+    opt = S.Adam(net.parameters(), lr=1e-3) if training else None
+    losses = []
+    for _ in range(epochs):
+        for b0 in range(0, xs.shape[0], bs):
+            x, lab = xs[b0:b0 + bs], ls[b0:b0 + bs]
+            o, s, a = net(x)
+            loss = loss_A(a, lab) + S.calc_selective_risk_image_b(o, s, target=lab, lamb=lamb)[0]
+            if training:
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+            for m in metrics:
+                m.add_batch(o.detach(), lab, s.detach())
+            losses.append(float(loss.item()))
+    return np.array(losses)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 0.002), (torch.bfloat16, 0.01)])
+def test_miou_parity_vs_reference_training(dtype, tol):
+    d = G.load("miou_sel_64.npz")
+    size, bs, ep, lamb = int(d["meta_size"]), int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
+    xtr, ltr = preprocess(*make_patches(int(d["meta_n_train"]), size, seed=int(d["meta_train_seed"])))
+    xva, lva = preprocess(*make_patches(int(d["meta_n_val"]), size, seed=int(d["meta_val_seed"])))
+    net = build(True, int(d["meta_seed"]), dtype)
+    tr = SegMetrics(DEV, selective=True, rule="train")
+    losses = _loop(net, torch.tensor(xtr, device=DEV), torch.tensor(ltr, device=DEV), bs, ep, lamb, True, [tr])
+    ref_losses = d["train_losses"]
+    print(f"train loss {losses[0]:.5f}->{losses[-1]:.5f} (reference {ref_losses[0]:.5f}->{ref_losses[-1]:.5f})")
+    assert abs(losses[0] - ref_losses[0]) < (1e-4 if dtype == torch.float32 else 2e-2) * abs(ref_losses[0])
+    assert np.abs(losses - ref_losses).max() < 0.05 * max(1.0, np.abs(ref_losses).max())
+    tr_cm = tr.confusion_matrix()
+    assert abs(mean_iou(tr_cm) - mean_iou(d["train_cm"])) <= tol
+    net.eval()
+    vs, vp = SegMetrics(DEV, selective=True, rule="train"), SegMetrics(DEV, selective=False, rule="train")
+    with torch.no_grad():
+        _loop(net, torch.tensor(xva, device=DEV), torch.tensor(lva, device=DEV), bs, 1, lamb, False, [vs, vp])
+    m_sel, m_all = mean_iou(vs.confusion_matrix()), mean_iou(vp.confusion_matrix())
+    print(f"val mIoU {m_all:.5f} (reference {float(d['val_miou']):.5f}), selective {m_sel:.5f} "
+          f"(reference {float(d['val_miou_selective']):.5f})")
+    assert abs(m_all - float(d["val_miou"])) <= tol
+    assert abs(m_sel - float(d["val_miou_selective"])) <= tol
+
+
+def _cli(tmp, *extra):
+    cmd = [sys.executable, "-m", "selectivenet_for_semantic_segmentation_binary_amd.train", "--data_dir",
+           "synthetic:40", "--patch_size", "64", "--model_arch", "UNet_B", "--loss", "BCElogit", "--selective", "1",
+           "--batch_size", "8", "--model_dir", str(tmp), "--steps_per_epoch", "3", "--val_steps", "1", *extra]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_train_cli_epochs_checkpoints_resume(tmp_path):
+    out = _cli(tmp_path, "--n_epoch", "2", "--lr_sche", "StepLR", "--patience", "1")
+    assert "train_loss" in out and "train_rejection" in out and "valid_rejection" in out
+    ck = tmp_path / "1-fold" / "checkpoint"
+    assert sorted(os.listdir(ck)) == ["model_epoch1.pth", "model_epoch2.pth"]
+    sd = torch.load(ck / "model_epoch2.pth", map_location="cpu", weights_only=True)
+    assert list(sd["net"].keys()) == S.state_dict_keys("RGB", True)
+    assert int(sd["net"]["encoder_layer_1_1.1.num_batches_tracked"]) == 6
+    assert len(sd["optim"]["state"]) == len(sd["net"]) - 3 * 14  # params only (no BN buffers)
+    hist = json.load(open(tmp_path / "1-fold" / "log" / "history.json"))
+    assert [h["epoch"] for h in hist] == [1, 2]
+    assert all(sum(map(sum, h["train_cm"])) > 0 for h in hist)
+    # resume: the newest checkpoint's weights, epoch numbering continues (train.py:113-127)
+    out2 = _cli(tmp_path, "--n_epoch", "1")
+    assert "Load weights from" in out2 and "epoch 3 / 3" in out2
+    assert sorted(os.listdir(ck))[-1] == "model_epoch3.pth"

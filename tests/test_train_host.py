@@ -1,0 +1,111 @@
+"""Host logic of the training loop (no GPU): metric thresholds, CLI flags, batch planning, splits."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import unet_b_cpu as O
+from selectivenet_for_semantic_segmentation_binary_amd import data as D
+from selectivenet_for_semantic_segmentation_binary_amd import parallel
+from selectivenet_for_semantic_segmentation_binary_amd.metrics import logit_threshold, mean_iou
+from selectivenet_for_semantic_segmentation_binary_amd.train import parse_arguments
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_thresholds_match_reference_constants():
+    kat = json.load(open(os.path.join(HERE, "golden", "kat.json")))
+    assert np.float32(logit_threshold("train")) == np.float32(kat["train_threshold_fp32_logit"])
+    assert np.float32(logit_threshold("eval")) == np.float32(kat["eval_threshold_fp32_logit"])
+
+
+@pytest.mark.parametrize("rule,cut", [("train", 0.5), ("eval", 0.5), ("eval", 0.3), ("eval", 0.9)])
+def test_threshold_equals_reference_rule(rule, cut):
+    """pred(x) == (x >= t) over a dense sweep around t and over random logits."""
+    t = np.float32(logit_threshold(rule, cut))
+    near = t.view(np.int32) + np.arange(-2000, 2000, dtype=np.int32)
+    rng = np.random.Generator(np.random.PCG64(3))
+    xs = np.concatenate([near.view(np.float32), rng.normal(0, 5, 20000).astype(np.float32),
+                         np.array([0.0, -0.0, np.inf, -np.inf, 1e30, -1e30], np.float32)])
+    with np.errstate(over="ignore"):
+        ref = O.train_pred_mask(xs) if rule == "train" else O.eval_pred_mask(xs, cut)
+    assert np.array_equal(ref, (xs >= t).astype(np.uint8))
+
+
+def test_miou_formula_matches_kat():
+    kat = json.load(open(os.path.join(HERE, "golden", "kat.json")))
+    assert abs(mean_iou(np.array(kat["cm"], np.float64)) - kat["miou"]) < 1e-12
+
+
+def test_cli_flags_mirror_reference():
+    a = parse_arguments([])
+    # train.py:12-55 defaults
+    assert (a.data_dir, a.fold, a.input_type, a.patch_mag, a.patch_size, a.n_cls) == ("/data", 1, "RGB", 200, 256, 2)
+    assert (a.model_dir, a.model_arch, a.selective, a.s_lamb, a.output_dim, a.output_scale) == \
+        ("/model", "UNet", False, 2, "NHW", "sigmoid")
+    assert (a.optim, a.momentum, a.w_decay, a.lr, a.lr_sche) == ("Adam", 0, 0, 1e-3, None)
+    assert (a.patience, a.factor, a.lr_min, a.loss, a.batch_size, a.n_epoch, a.local_rank, a.log_img) == \
+        (10, 0.5, 1e-5, "CE", 16, 100, [0], False)
+    # train.sh; argparse type=bool: '--selective 0' is True
+    b = parse_arguments("--fold 1 --data_dir /data --model_dir /model --model_arch UNet_B --selective 0 "
+                        "--loss BCElogit --local_rank 0 1 2 3 4 5 6 7 --n_epoch 200 --batch_size 128".split())
+    assert b.selective is True and b.local_rank == list(range(8)) and b.batch_size == 128
+
+
+def _plan(n, bs, world, rank):
+    parallel._STATE.update(enabled=True, group=None)
+    try:
+        import torch.distributed as dist
+        orig = (dist.is_initialized, dist.get_world_size, dist.get_rank)
+        dist.is_initialized = lambda: True
+        dist.get_world_size = lambda group=None: world
+        dist.get_rank = lambda group=None: rank
+        ds = D.PatchSet(np.zeros((n, 8, 8, 3), np.uint8), np.zeros((n, 8, 8), np.uint8))
+        ld = D.BatchLoader(ds, bs, shuffle=True, random_flip=True, device="cpu", seed=7)
+        ld.set_epoch(3)
+        return ld._plan(), ld.dropped
+    finally:
+        dist.is_initialized, dist.get_world_size, dist.get_rank = orig
+        parallel.disable()
+
+
+def test_batch_plan_chunks_agree_across_ranks():
+    n, bs, world = 45, 16, 4
+    plans = [_plan(n, bs, world, r) for r in range(world)]
+    # every rank drops the same batches; together the ranks cover each kept global batch exactly once
+    assert len({len(p) for p, _ in plans}) == 1
+    for b in range(len(plans[0][0])):
+        rows = np.concatenate([plans[r][0][b][1] for r in range(world)])
+        assert plans[0][0][b][0] == len(rows)
+        assert len(set(rows.tolist())) == len(rows)
+    # 45 = 16 + 16 + 13: 13 over 4 ranks = chunks of 4,4,4,1 -> kept
+    assert plans[0][1] == 0 and sum(len(plans[r][0][2][1]) for r in range(world)) == 13
+
+
+def test_batch_plan_drops_batch_that_leaves_a_rank_empty():
+    # last batch of 5 over 4 ranks: torch.chunk -> 2,2,1 (3 chunks) -> rank 3 would be empty
+    plans = [_plan(21, 16, 4, r) for r in range(4)]
+    assert all(len(p) == 1 and d == 1 for p, d in plans)
+
+
+def test_construct_train_valid_matches_reference_split(tmp_path):
+    """utils/data_utils.py:49-76 with its module-level np.random.seed(42), restated inline."""
+    for f in range(1, 6):
+        tum = np.array([[f"s{f}_{i}_input.jpg", f"s{f}_{i}_label.png"] for i in range(7 + f)])
+        non = np.array([[f"n{f}_{i}_input.jpg", f"n{f}_{i}_label.png"] for i in range(11 + f)])
+        np.save(tmp_path / f"{f}-fold_tumorable_data.npy", tum)
+        np.save(tmp_path / f"{f}-fold_non_tumorable_data.npy", non)
+    train, valid = D.construct_train_valid(str(tmp_path), test_fold=2)
+    np.random.seed(42)
+    tum = np.concatenate([np.load(tmp_path / f"{i}-fold_tumorable_data.npy") for i in (1, 3, 4, 5)])
+    non = np.concatenate([np.load(tmp_path / f"{i}-fold_non_tumorable_data.npy") for i in (1, 3, 4, 5)])
+    out = []
+    for lst in (tum, non):
+        vi = np.random.choice(len(lst), size=int(len(lst) * 0.2), replace=False)
+        ti = np.setdiff1d(list(range(len(lst))), vi)
+        out.append((lst[ti], lst[vi]))
+    assert np.array_equal(train, np.vstack([out[0][0], out[1][0]]))
+    assert np.array_equal(valid, np.vstack([out[0][1], out[1][1]]))
+    test = D.construct_test(str(tmp_path), test_fold=2)
+    assert len(test) == 9 + 13
