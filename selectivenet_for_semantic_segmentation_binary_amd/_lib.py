@@ -102,7 +102,8 @@ _lock = threading.Lock()
 
 
 def lib_path() -> str:
-    return _build.LIB
+    """The in-tree build; SELUNET_LIB overrides it (A/B timing of kernel variants)."""
+    return os.environ.get("SELUNET_LIB", _build.LIB)
 
 
 def load(auto_build: bool = False):

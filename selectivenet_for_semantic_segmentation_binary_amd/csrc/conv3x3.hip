@@ -9,8 +9,8 @@
 // one tap x one 128-B channel chunk (32 fp32 / 64 bf16 channels). B (weights) is double-buffered
 // per step; the next chunk's halo is loaded a 16-B slice per thread per tap during the current
 // chunk's first six taps (load early, write late) into the second halo buffer.
-// LDS rows are 144 B (128 B + 16 B pad) so ds_read_b128 fragment reads of 16 consecutive rows hit
-// 16 distinct bank slots.
+// Weight rows in LDS are 144 B (128 B + 16 B pad) so ds_read_b128 fragment reads of 16 consecutive
+// rows hit 16 distinct bank slots; halo rows use the swizzled 160-B layout below (AROWB).
 #include <cstdlib>
 
 #include "gemm_common.h"
@@ -22,6 +22,12 @@ constexpr int HHT = TH + 2, HWT = TW + 2;  // halo tile
 constexpr int HPIX = HHT * HWT;         // 324 halo pixels
 constexpr int HTHREADS = 512;
 constexpr int A_ROUNDS = (HPIX * 8 + HTHREADS - 1) / HTHREADS;  // 16-B halo loads per thread per chunk
+// Halo rows are 160 B (10 bank units of 16 B) with the two 16-B halves of each 32-B k slice
+// swapped on odd halo lines (slot ^ (hy & 1)): the fragment reads of a wave's 32 pixels (two image
+// rows, i.e. halo rows R..R+15 and R+18..R+33) then hit 16 distinct bank units in every ds_read_b128
+// lane group for all nine tap offsets (144-B rows: 2-way conflicts on this pattern).
+constexpr int AROWB = 160;
+__device__ __forceinline__ int halo_off(int hp, int cc) { return hp * AROWB + ((cc ^ ((hp / HWT) & 1)) << 4); }
 
 // ONE_CHUNK: the whole K of a tap fits one chunk (C == CK): a single halo buffer, no halo
 // prefetch, and LDS small enough for two workgroups per CU so one's prologue/epilogue overlaps
@@ -42,11 +48,11 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
   constexpr int NHBUF = ONE_CHUNK ? 1 : 2;
   constexpr int AD = 3;                   // halo slice loaded at tap r is written at tap r + AD
 
-  constexpr int SMEM_MAIN = NHBUF * HPIX * ROWB + 2 * BN * ROWB + (ONE_CHUNK ? 0 : 2 * CK * 8);
+  constexpr int SMEM_MAIN = NHBUF * HPIX * AROWB + 2 * BN * ROWB + (ONE_CHUNK ? 0 : 2 * CK * 8);
   constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
   unsigned char* As = smem;
-  unsigned char* Bs = smem + NHBUF * HPIX * ROWB;
+  unsigned char* Bs = smem + NHBUF * HPIX * AROWB;
   // folded BN coefficients of the prefetched chunk: [2 buffers][CK] scale, then [2][CK] shift
   float* Ss = reinterpret_cast<float*>(Bs + 2 * BN * ROWB);
 
@@ -123,16 +129,18 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
 
-  // per-lane halo row of pixel (subtile a, lane) for tap (0,0)
-  int hrow0[MT];
+  // per-lane halo row of pixel (subtile a, lane) for tap (0,0), and the 16-B half it reads after the
+  // odd-line swap (half ^ parity of the halo line; the tap's dy flips the parity)
+  int hrow0[MT], hsw0[MT];
 #pragma unroll
   for (int a = 0; a < MT; ++a) {
     const int pix = wm * WPIX + a * 32 + l32;
     hrow0[a] = (pix / TW) * HWT + (pix % TW);
+    hsw0[a] = half ^ ((pix / TW) & 1);
   }
 
   auto mma_step = [&](int hbuf, int bbuf, int t) __attribute__((always_inline)) {
-    const unsigned char* a_src = As + hbuf * HPIX * ROWB;
+    const unsigned char* a_src = As + hbuf * HPIX * AROWB;
     const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
@@ -141,7 +149,8 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
       const int boff = q * 32 + half * 16;
       uint4 af[MT], bfr[NT];
 #pragma unroll
-      for (int a = 0; a < MT; ++a) af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * ROWB + boff);
+      for (int a = 0; a < MT; ++a)
+        af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
 #pragma unroll
       for (int b = 0; b < NT; ++b)
         bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
@@ -172,7 +181,7 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
         v = v0[r];
         if (sa.scale) v = transform16<T>(v, sa.scale, sa.shift, c0 + cc * E, sa.relu);
       }
-      *reinterpret_cast<uint4*>(As + hp * ROWB + cc * 16) = v;
+      *reinterpret_cast<uint4*>(As + halo_off(hp, cc)) = v;
     }
   }
   BRegs rb_next = b_load(0);
@@ -236,7 +245,7 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
                 __builtin_memcpy(&v, e, 16);
               }
             }
-            *reinterpret_cast<uint4*>(As + (((c + 1) & 1) * HPIX + hp) * ROWB + cc * 16) = v;
+            *reinterpret_cast<uint4*>(As + ((c + 1) & 1) * HPIX * AROWB + halo_off(hp, cc)) = v;
           }
         }
         __syncthreads();

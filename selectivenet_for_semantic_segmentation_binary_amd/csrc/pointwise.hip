@@ -115,13 +115,30 @@ __global__ void reduce_rows_l1(const float* __restrict__ slab, int64_t rows, int
     ws[(int64_t)blockIdx.y * cols + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
+// 4 split lanes x 64 columns per block; each lane sums every 4th split (8 independent loads in
+// flight), then the 4 lane sums are added in a fixed order: deterministic, and latency-bound work
+// spread over 4x the threads of a one-thread-per-column loop.
 __global__ void reduce_rows_l2(const double* __restrict__ ws, int splits, int cols, double* out, float* out32) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= cols) return;
-  double acc = 0.0;
-  for (int s = 0; s < splits; ++s) acc += ws[(int64_t)s * cols + col];
-  if (out) out[col] = acc;
-  if (out32) out32[col] = (float)acc;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6;
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < cols) {
+    int s = sl;
+    for (; s + 28 < splits; s += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += ws[(int64_t)(s + 4 * u) * cols + col];
+    }
+    for (; s < splits; s += 4) acc[0] += ws[(int64_t)s * cols + col];
+  }
+  double t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __shared__ double red[4][64];
+  red[sl][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (sl == 0 && col < cols) {
+    const double v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    if (out) out[col] = v;
+    if (out32) out32[col] = (float)v;
+  }
 }
 
 int64_t channel_slab_rows(int64_t m) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(m, 256), 2048)); }
@@ -733,7 +750,7 @@ int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* w
   const int64_t chunk = cdiv(rows, splits);
   hipLaunchKernelGGL(reduce_rows_l1, dim3((unsigned)cdiv(cols, 64), splits), dim3(TPB), 0, as_stream(stream), slab,
                      rows, cols, chunk, ws);
-  hipLaunchKernelGGL(reduce_rows_l2, dim3((unsigned)cdiv(cols, TPB)), dim3(TPB), 0, as_stream(stream), ws, splits,
+  hipLaunchKernelGGL(reduce_rows_l2, dim3((unsigned)cdiv(cols, 64)), dim3(TPB), 0, as_stream(stream), ws, splits,
                      cols, out, out32);
   return check_launch("reduce_rows");
 }
