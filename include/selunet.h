@@ -175,6 +175,12 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
                          const float* shift, const float* mean, const float* invstd,
                          const float* coef, void* dy, int32_t dtype, void* stream);
 
+/* Stream-ordered device memset / device-to-device copy (hipMemsetAsync / hipMemcpyAsync):
+ * zeroing atomic-accumulation targets and gathering small parameter vectors inside a recorded
+ * launch plan, without host synchronisation. */
+int selunet_memset(void* dst, int32_t value, int64_t bytes, void* stream);
+int selunet_memcpy(void* dst, const void* src, int64_t bytes, void* stream);
+
 /* ---- first layer (C_in = 3 or 2, model.py:24-29) --------------------------------------- */
 /* x NCHW fp32 -> out [n*h*w][k_pad] in dtype: column tap*c + ci of the 3x3 pad-1 window, zero
  * for columns >= 9c. The first conv then runs as selunet_gemm_gather with taps = 1. */

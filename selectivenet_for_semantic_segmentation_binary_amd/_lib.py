@@ -93,6 +93,8 @@ SIGNATURES = {
     "selunet_bce_finalize": (c_int32, [P, c_double, P, P]),
     "selunet_bce_bwd": (c_int32, [P, P, c_int64, c_double, P, P, P]),
     "selunet_adam_step": (c_int32, [P, c_int32, c_int64, c_float, c_float, c_float, c_float, c_float, c_int64, P]),
+    "selunet_memset": (c_int32, [P, c_int32, c_int64, P]),
+    "selunet_memcpy": (c_int32, [P, P, c_int64, P]),
     "selunet_prep_batch": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
     "selunet_seg_metrics": (c_int32, [P, P, P, c_int64, c_float, c_float, P, P]),
 }
@@ -148,10 +150,111 @@ def set_call_hook(hook):
 def call(name, *args):
     L = load()
     fn = getattr(L, name)
+    if _REC is not None:
+        _REC.record(name, fn, args)
     rc = fn(*args) if _HOOK is None else _HOOK(name, args, lambda: fn(*args))
     if rc != 0:
         raise SelunetError(f"{name}: {L.selunet_last_error().decode()}")
     return rc
+
+
+# ----------------------------------------------------------------------------- launch plans
+class Slot:
+    """A recorded pointer argument that points into a per-call buffer: rebound at replay."""
+    __slots__ = ("name", "offset")
+
+    def __init__(self, name, offset):
+        self.name, self.offset = name, offset
+
+
+class Plan:
+    """The exact sequence of C-ABI calls one engine pass made, with their (already converted)
+    arguments. Replaying it re-issues the same launches without re-running the Python sequencing
+    (allocation, descriptor building, queries): the host cost of a step drops to the ctypes calls.
+    Pointer arguments that fall inside a registered per-call buffer (the network input, the head
+    outputs, the incoming head gradients, the gradient buffer) are recorded as Slots and rebound
+    to that call's buffers; every other pointer refers to memory the plan owns."""
+
+    def __init__(self, slots):
+        self._ranges = [(n, t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for n, t in slots.items()
+                        if t is not None]
+        self.calls = []  # (name, fn, args, slot_positions)
+        self.keep = []   # every buffer the recorded calls touch stays allocated for the plan's life
+
+    def _slot(self, v):
+        if isinstance(v, int) and v:
+            for n, lo, hi in self._ranges:
+                if lo <= v < hi:
+                    return Slot(n, v - lo)
+        return None
+
+    def record(self, name, fn, args):
+        args = list(args)
+        pos = []
+        for i, a in enumerate(args):
+            if isinstance(a, ctypes.Structure):
+                _check_struct(a, self._slot, name)
+                continue
+            sl = self._slot(a)
+            if sl is not None:
+                args[i] = sl
+                pos.append(i)
+        self.calls.append((name, fn, tuple(args), tuple(pos)))
+
+    def replay(self, slots):
+        base = {n: t.data_ptr() for n, t in slots.items() if t is not None}
+        L = load()
+        for name, fn, args, pos in self.calls:
+            if pos:
+                a = list(args)
+                for i in pos:
+                    a[i] = base[a[i].name] + a[i].offset
+                args = a
+            rc = fn(*args) if _HOOK is None else _HOOK(name, args, lambda fn=fn, args=args: fn(*args))
+            if rc != 0:
+                raise SelunetError(f"{name}: {L.selunet_last_error().decode()}")
+
+
+def _check_struct(st, slot_of, name):
+    for f, _ in st._fields_:
+        v = getattr(st, f)
+        if isinstance(v, ctypes.Structure):
+            _check_struct(v, slot_of, name)
+        elif isinstance(v, ctypes.Array):
+            for e in v:
+                if isinstance(e, ctypes.Structure):
+                    _check_struct(e, slot_of, name)
+        elif slot_of(v) is not None:
+            raise RuntimeError(f"{name}: a per-call buffer is referenced inside a descriptor; it cannot be replayed")
+
+
+_REC = None
+
+
+def keep(t):
+    """Allocation made by recorded sequencing: owned by the plan being recorded (if any)."""
+    if _REC is not None and t is not None:
+        _REC.keep.append(t)
+    return t
+
+
+class recording:
+    """Context manager: record every `call` made inside into `plan`."""
+
+    def __init__(self, plan):
+        self.plan = plan
+
+    def __enter__(self):
+        global _REC
+        if _REC is not None:
+            raise RuntimeError("nested plan recording")
+        _REC = self.plan
+        return self.plan
+
+    def __exit__(self, *exc):
+        global _REC
+        _REC = None
+        return False
 
 
 def query(name, *args):

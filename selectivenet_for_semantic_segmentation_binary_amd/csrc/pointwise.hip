@@ -741,6 +741,20 @@ int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float
   return check_launch("unpack_convT_grad");
 }
 
+int selunet_memset(void* dst, int32_t value, int64_t bytes, void* stream) {
+  SELUNET_REQUIRE(dst && bytes >= 0, "memset: bad arguments");
+  if (bytes && hipMemsetAsync(dst, value, (size_t)bytes, as_stream(stream)) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipMemsetAsync failed");
+  return 0;
+}
+
+int selunet_memcpy(void* dst, const void* src, int64_t bytes, void* stream) {
+  SELUNET_REQUIRE(dst && src && bytes >= 0, "memcpy: bad arguments");
+  if (bytes && hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, as_stream(stream)) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipMemcpyAsync failed");
+  return 0;
+}
+
 int64_t selunet_reduce_ws_bytes(int32_t cols) { return (int64_t)RED_SPLITS * cols * (int64_t)sizeof(double); }
 
 int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* ws, double* out, float* out32,

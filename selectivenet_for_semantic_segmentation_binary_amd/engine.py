@@ -13,6 +13,9 @@ bottleneck -> pool3 backward (+ d(skip3)) -> enc3_2 -> ... -> enc1_1 (no data gr
 """
 from __future__ import annotations
 
+import os
+import weakref
+from collections import OrderedDict
 from dataclasses import dataclass, field
 
 import torch
@@ -66,23 +69,49 @@ class Ctx:
     selective: bool
     shape: tuple
     x: torch.Tensor = None
+    entry: object = None     # the launch-plan cache entry this context belongs to (None: uncached)
     bn: dict = field(default_factory=dict)
     pools: dict = field(default_factory=dict)
     ups: dict = field(default_factory=dict)
     wpack: dict = field(default_factory=dict)
 
 
+class _Entry:
+    """One recorded forward (and its backward plans) with the activations it owns."""
+
+    def __init__(self, key):
+        self.key = key
+        self.plan = None
+        self.ctx = None
+        self.bwd = {}
+        self.busy = False
+
+
 class Engine:
-    """Stateless sequencer; parameters/buffers are passed in as dicts of tensors."""
+    """Sequencer; parameters/buffers are passed in as dicts of tensors.
+
+    Launch plans: the first forward (and backward) for a given input shape / mode / parameter set
+    runs the Python sequencing below while recording every C-ABI call (`_lib.Plan`); later calls
+    with the same signature replay the recorded launches with the per-call buffers (input, head
+    outputs, head gradients, gradient buffer) rebound, so the host cost of a training step is the
+    ctypes calls alone — what keeps small per-GPU batches (8-GPU strong scaling) GPU-bound. The
+    activations a plan owns stay allocated between steps (the caching allocator would have held
+    them anyway); a forward whose backward is pending keeps its plan busy, and a second forward of
+    the same shape then records (or, past MAX_PLANS, runs unrecorded). SELUNET_NO_PLANS=1 disables
+    plans."""
+
+    MAX_PLANS = 4  # per signature
 
     def __init__(self, dt: torch.dtype = torch.float32):
         self.dt = dt
         self.code = K.dtype_code(dt)
         self.bke = 128 // torch.empty((), dtype=dt).element_size()
+        self.plans_enabled = os.environ.get("SELUNET_NO_PLANS", "0") != "1"
+        self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
     def _reduce(self, slab, rows, cols, out64=None, out32=None):
-        ws = torch.empty(K.query("selunet_reduce_ws_bytes", cols) // 8, dtype=torch.float64, device=slab.device)
+        ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", cols) // 8, dtype=torch.float64, device=slab.device))
         K.call("selunet_reduce_rows", K.ptr(slab), rows, cols, K.ptr(ws), K.ptr(out64), K.ptr(out32), self.stream)
 
     @property
@@ -97,16 +126,16 @@ class Engine:
             w = P[f"{name}.0.weight"]
             ci = w.shape[1]
             kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
-            fwd = torch.empty(co, kpad, dtype=self.dt, device=dev)
+            fwd = K.keep(torch.empty(co, kpad, dtype=self.dt, device=dev))
             dg = None
             if need_dgrad and name != "encoder_layer_1_1":
-                dg = torch.empty(ci, 9 * co, dtype=self.dt, device=dev)
+                dg = K.keep(torch.empty(ci, 9 * co, dtype=self.dt, device=dev))
             K.call("selunet_pack_conv3x3", K.ptr(w), co, ci, kpad, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
             packs[name] = (fwd, dg, kpad)
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
-            fwd = torch.empty(4 * co, ci, dtype=self.dt, device=dev)
-            dg = torch.empty(ci, 4 * co, dtype=self.dt, device=dev) if need_dgrad else None
+            fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
+            dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
             K.call("selunet_pack_convT", K.ptr(w), ci, co, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
             packs[name] = (fwd, dg, ci)
         return packs
@@ -119,7 +148,7 @@ class Engine:
         co = fwd.shape[0]
         M = n * h * w
         dev = fwd.device
-        y = torch.empty(M, co, dtype=self.dt, device=dev)
+        y = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         stats = None
         if first_x is not None:
             rows = K.query("selunet_first_conv_rows", n, h, w)
@@ -127,17 +156,17 @@ class Engine:
             g = K.gather(n, h, w, taps, *srcs)
             rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
         if ctx.training:
-            stats = torch.empty(rows, 2, co, dtype=torch.float32, device=dev)
+            stats = K.keep(torch.empty(rows, 2, co, dtype=torch.float32, device=dev))
         if first_x is not None:
             K.call("selunet_first_conv_fwd", K.ptr(first_x), n, first_x.shape[1], h, w, K.ptr(fwd), K.ptr(y),
                    K.ptr(stats), self.code, self.stream)
         else:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
             K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
-        mean, invstd, scale, shift = (torch.empty(co, dtype=torch.float32, device=dev) for _ in range(4))
+        mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
         sums = None
         if ctx.training:
-            sums = torch.empty(2 * co, dtype=torch.float64, device=dev)
+            sums = K.keep(torch.empty(2 * co, dtype=torch.float64, device=dev))
             self._reduce(stats, rows, 2 * co, out64=sums)
         K.call("selunet_bn_finalize", K.ptr(sums), M, co, K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]),
                K.ptr(P[f"{name}.1.bias"]), K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
@@ -148,7 +177,7 @@ class Engine:
         return st
 
     def _pool(self, ctx, key, st: BNState):
-        out = torch.empty(st.n * (st.h // 2) * (st.w // 2), st.c, dtype=self.dt, device=st.y.device)
+        out = K.keep(torch.empty(st.n * (st.h // 2) * (st.w // 2), st.c, dtype=self.dt, device=st.y.device))
         K.call("selunet_maxpool2_fwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(out), self.code, self.stream)
         ctx.pools[key] = out
@@ -157,19 +186,74 @@ class Engine:
     def _up(self, ctx, name, P, st: BNState):
         fwd, _, ci = ctx.wpack[name]
         co = fwd.shape[0] // 4
-        out = torch.empty(st.n * 2 * st.h * 2 * st.w, co, dtype=self.dt, device=st.y.device)
+        out = K.keep(torch.empty(st.n * 2 * st.h * 2 * st.w, co, dtype=self.dt, device=st.y.device))
         g = K.gather(st.n, st.h, st.w, 1, st.src())
         ep = K.Epilogue(K.ptr(out), None, K.ptr(P[f"{name}.bias"]), None, K.EP_SCATTER2X, 0)
         K.call("selunet_gemm_gather", g, K.ptr(fwd), 4 * co, ci, ep, self.code, self.stream)
         ctx.ups[name] = out
         return out
 
+    # ------------------------------------------------------------------ plan cache
+    def _signature(self, x, P, B, selective, training, need_backward):
+        return (tuple(x.shape), x.device.index, bool(selective), bool(training), bool(need_backward), self.stream,
+                tuple(t.data_ptr() for t in P.values()), tuple(t.data_ptr() for t in B.values()))
+
+    def _entry_for(self, sig):
+        lst = self._plans.get(sig)
+        if lst is None:
+            lst = self._plans[sig] = []
+            while len(self._plans) > 2 * self.MAX_PLANS:  # evict the oldest signature with no busy entry
+                for k, v in self._plans.items():
+                    if k != sig and not any(e.busy for e in v):
+                        del self._plans[k]
+                        break
+                else:
+                    break
+        self._plans.move_to_end(sig)
+        for e in lst:
+            if not e.busy:
+                return e
+        if len(lst) < self.MAX_PLANS:
+            e = _Entry(sig)
+            lst.append(e)
+            return e
+        return None
+
+    @staticmethod
+    def release(ctx):
+        """Mark the plan of a forward whose backward will not run (autograd graph freed) reusable."""
+        if ctx is not None and ctx.entry is not None:
+            ctx.entry.busy = False
+
     def forward(self, x, P, B, selective, training, need_backward=False):
-        """x: [N, Cin, H, W] fp32 contiguous. Returns (heads tuple, ctx)."""
+        """x: [N, Cin, H, W] fp32 contiguous. Returns (heads tuple, ctx); the heads are new tensors."""
         assert x.dim() == 4 and x.is_contiguous() and x.dtype == torch.float32
         n, cin, H, W = x.shape
         if H % 8 or W % 8:
             raise ValueError(f"UNet_B needs H and W divisible by 8 (three 2x2 poolings); got {H}x{W}")
+        nheads = 3 if selective else 1
+        outs = tuple(torch.empty(n, H, W, dtype=torch.float32, device=x.device) for _ in range(nheads))  # per call
+        e = self._entry_for(self._signature(x, P, B, selective, training, need_backward)) \
+            if self.plans_enabled else None
+        slots = {"x": x, **{f"out{i}": o for i, o in enumerate(outs)}}
+        if e is None:
+            ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs)
+        elif e.plan is not None:
+            e.plan.replay(slots)
+            ctx = e.ctx
+            ctx.x = x
+        else:
+            plan = K.Plan(slots)
+            with K.recording(plan):
+                ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs)
+            e.plan, e.ctx = plan, ctx
+            ctx.entry = e
+        if e is not None and training and need_backward:
+            e.busy = True
+        return outs, ctx
+
+    def _forward_impl(self, x, P, B, selective, training, need_backward, outs):
+        n, cin, H, W = x.shape
         ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
@@ -197,14 +281,16 @@ class Engine:
         d11 = c("decoder_layer_1_1", h1, w1, d12.src())
         M = n * H * W
         heads = LY.HEADS if selective else LY.HEADS[:1]
-        hw = torch.cat([P[f"{h}.weight"].reshape(1, 64) for h in heads]).contiguous()
-        hb = torch.cat([P[f"{h}.bias"].reshape(1) for h in heads]).contiguous()
-        outs = [torch.empty(n, H, W, dtype=torch.float32, device=x.device) for _ in heads]
-        o = outs + [None] * (3 - len(outs))
+        hw = K.keep(torch.empty(len(heads), 64, dtype=torch.float32, device=x.device))
+        hb = K.keep(torch.empty(len(heads), dtype=torch.float32, device=x.device))
+        for i, h in enumerate(heads):  # the heads' current weights, gathered in stream order
+            K.call("selunet_memcpy", K.ptr(hw[i]), K.ptr(P[f"{h}.weight"]), 64 * 4, self.stream)
+            K.call("selunet_memcpy", K.ptr(hb[i:]), K.ptr(P[f"{h}.bias"]), 4, self.stream)
+        o = list(outs) + [None] * (3 - len(outs))
         K.call("selunet_heads_fwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(hw), K.ptr(hb),
                len(heads), K.ptr(o[0]), K.ptr(o[1]), K.ptr(o[2]), self.code, self.stream)
         ctx.head_w = hw
-        return tuple(outs), ctx
+        return ctx
 
     # ------------------------------------------------------------------ backward pieces
     def _cbr_bwd(self, ctx, name, dg: DGrad, G, input_srcs, dgrad_split=None, need_dgrad=True, q_taps=9,
@@ -215,31 +301,32 @@ class Engine:
         pair for a concatenated input (d(up) with its column sums)."""
         st: BNState = ctx.bn[name]
         M, co, dev = st.n * st.h * st.w, st.c, st.y.device
-        sums = torch.empty(3 * co, dtype=torch.float64, device=dev)
+        sums = K.keep(torch.empty(3 * co, dtype=torch.float64, device=dev))
         self._reduce(dg.slab, dg.rows, 3 * co, out64=sums)
-        coef = torch.empty(3, co, dtype=torch.float32, device=dev)
+        coef = K.keep(torch.empty(3, co, dtype=torch.float32, device=dev))
         gamma = ctx.params[f"{name}.1.weight"]
         K.call("selunet_bn_bwd_finalize", K.ptr(sums), M, co, K.ptr(gamma), K.ptr(st.invstd),
                K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]), K.ptr(coef),
                self.stream)
-        dy = torch.empty(M, co, dtype=self.dt, device=dev)
+        dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
         if first_x is not None:
             cin = first_x.shape[1]
             rows = K.query("selunet_first_conv_wgrad_rows", st.n, st.h, st.w)
-            slab = torch.empty(rows, co, FIRST_KPAD, dtype=torch.float32, device=dev)
+            slab = K.keep(torch.empty(rows, co, FIRST_KPAD, dtype=torch.float32, device=dev))
             K.call("selunet_first_conv_wgrad", K.ptr(first_x), st.n, cin, st.h, st.w, K.ptr(dy), K.ptr(slab),
                    self.code, self.stream)
-            packed = torch.empty(co, FIRST_KPAD, dtype=torch.float32, device=dev)
+            packed = K.keep(torch.empty(co, FIRST_KPAD, dtype=torch.float32, device=dev))
             self._reduce(slab, rows, co * FIRST_KPAD, out32=packed)
             K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, cin, FIRST_KPAD, K.ptr(G[f"{name}.0.weight"]),
                    self.stream)
             return None
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
-        packed = torch.zeros(co, ld, dtype=torch.float32, device=dev)
+        packed = K.keep(torch.empty(co, ld, dtype=torch.float32, device=dev))
+        K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
         K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
@@ -250,18 +337,18 @@ class Engine:
         ga = K.gather(st.n, st.h, st.w, 9, K.source(dy, co))
         rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
         if dgrad_split is None:
-            dx = torch.empty(M, ci, dtype=self.dt, device=dev)
+            dx = K.keep(torch.empty(M, ci, dtype=self.dt, device=dev))
             ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
             slab = None
             if prev is not None:
-                slab = torch.empty(rows, 3, ci, dtype=torch.float32, device=dev)
+                slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
                 ep.bnb = bnb_for(prev, slab)
             K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
             return DGrad(dx, slab, rows)
         c0 = dgrad_split
-        d0 = torch.empty(M, c0, dtype=self.dt, device=dev)
-        d1 = torch.empty(M, ci - c0, dtype=self.dt, device=dev)
-        colsum = torch.empty(rows, c0, dtype=torch.float32, device=dev)
+        d0 = K.keep(torch.empty(M, c0, dtype=self.dt, device=dev))
+        d1 = K.keep(torch.empty(M, ci - c0, dtype=self.dt, device=dev))
+        colsum = K.keep(torch.empty(rows, c0, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0, K.ptr(colsum))
         K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
         return DGrad(d0, colsum, rows), d1
@@ -275,55 +362,78 @@ class Engine:
         dev = du.t.device
         self._reduce(du.slab, du.rows, co, out32=G[f"{name}.bias"])
         ld = K.query("selunet_wgrad_ld", 4 * co)
-        packed = torch.zeros(ci, ld, dtype=torch.float32, device=dev)
+        packed = K.keep(torch.empty(ci, ld, dtype=torch.float32, device=dev))
+        K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
         gp = K.gather(n, h, w, 1, prev.src())
         gq = K.gather(n, h, w, 4, K.source(du.t, co))
         K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
         K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
-        dz = torch.empty(n * h * w, ci, dtype=self.dt, device=dev)
+        dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))
         rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
-        slab = torch.empty(rows, 3, ci, dtype=torch.float32, device=dev)
+        slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = bnb_for(prev, slab)
         K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
         return DGrad(dz, slab, rows)
 
     def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
-        dz = torch.empty_like(st.y)
+        dz = K.keep(torch.empty_like(st.y))
         rows = K.query("selunet_maxpool2_bwd_slab_rows", st.n, st.h, st.w, st.c)
-        slab = torch.empty(rows, 3, st.c, dtype=torch.float32, device=dz.device)
+        slab = K.keep(torch.empty(rows, 3, st.c, dtype=torch.float32, device=dz.device))
         bnb = bnb_for(st, slab)
         K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(dp.t), K.ptr(dskip), K.ptr(dz), bnb, self.code, self.stream)
         return DGrad(dz, slab, rows)
 
-    def backward(self, ctx, P, G, g_heads):
-        """g_heads: list of fp32 [N,H,W] grads of (out[, select, aux]) (None -> zeros).
-        Writes every parameter gradient into the tensors of dict G (fp32, reference layouts)."""
+    def backward(self, ctx, P, G, g_heads, flat):
+        """g_heads: list of fp32 [N,H,W] grads of (out[, select, aux]) (None -> zeros). G: the
+        parameter-gradient views (reference layouts) of the flat fp32 buffer `flat`, written here."""
+        g_heads = [g.contiguous() if g is not None else None for g in g_heads]
+        e = ctx.entry
+        if e is None:
+            self._backward_impl(ctx, P, G, g_heads)
+            return
+        pattern = tuple(g is None for g in g_heads)
+        slots = {"x": ctx.x, "flat": flat, **{f"g{i}": g for i, g in enumerate(g_heads) if g is not None}}
+        plan = e.bwd.get(pattern)
+        try:
+            if plan is not None:
+                plan.replay(slots)
+            else:
+                plan = K.Plan(slots)
+                with K.recording(plan):
+                    self._backward_impl(ctx, P, G, g_heads)
+                e.bwd[pattern] = plan
+        finally:
+            e.busy = False
+
+    def _backward_impl(self, ctx, P, G, g_heads):
         ctx.params = P
         n, cin, H, W = ctx.shape
         M = n * H * W
         dev = ctx.x.device
         bn = ctx.bn
         heads = LY.HEADS if ctx.selective else LY.HEADS[:1]
-        gs = [g if g is not None else torch.zeros(n, H, W, dtype=torch.float32, device=dev) for g in g_heads]
-        gs = [g.contiguous() for g in gs] + [None] * (3 - len(gs))
+        gs = [g if g is not None else K.keep(torch.zeros(n, H, W, dtype=torch.float32, device=dev)) for g in g_heads]
+        gs = gs + [None] * (3 - len(gs))
         d11 = bn["decoder_layer_1_1"]
-        dz = torch.empty(M, 64, dtype=self.dt, device=dev)
+        dz = K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
         rows = K.query("selunet_channel_slab_rows", M)
         nh = len(heads)
-        slab = torch.empty(rows, nh * 65, dtype=torch.float32, device=dev)
-        bslab = torch.empty(rows, 3, 64, dtype=torch.float32, device=dev)
+        slab = K.keep(torch.empty(rows, nh * 65, dtype=torch.float32, device=dev))
+        bslab = K.keep(torch.empty(rows, 3, 64, dtype=torch.float32, device=dev))
         K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
                K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
                self.stream)
         dz = DGrad(dz, bslab, rows)
-        hsum = torch.empty(nh, 65, dtype=torch.float32, device=dev)
-        self._reduce(slab, rows, nh * 65, out32=hsum)
+        # head weight/bias grads are consecutive in the gradient buffer ([nh][64 + 1], registration
+        # order conv1x1, conv_select, conv_aux): reduce straight into it
+        hw0 = G[f"{heads[0]}.weight"]
         for i, h in enumerate(heads):
-            G[f"{h}.weight"].view(64).copy_(hsum[i, :64])
-            G[f"{h}.bias"].view(1).copy_(hsum[i, 64:])
+            assert G[f"{h}.weight"].data_ptr() == hw0.data_ptr() + i * 65 * 4
+            assert G[f"{h}.bias"].data_ptr() == hw0.data_ptr() + (i * 65 + 64) * 4
+        self._reduce(slab, rows, nh * 65, out32=hw0)
 
         e12, e22, e32 = bn["encoder_layer_1_2"], bn["encoder_layer_2_2"], bn["encoder_layer_3_2"]
         u1, u2, u3 = ctx.ups["unpool1"], ctx.ups["unpool2"], ctx.ups["unpool3"]

@@ -14,6 +14,7 @@ statistics, losses and master weights).
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 import torch.nn as nn
@@ -101,6 +102,8 @@ class _UNetBFunction(torch.autograd.Function):
             ctx.eng = eng
             ctx.names = names
             ctx.P = P
+            # a graph freed without backward must hand the engine's launch plan back
+            ctx.release = weakref.finalize(ctx, Engine.release, ectx)
         else:
             ctx.ectx = None
         return outs if len(outs) > 1 else outs[0]
@@ -118,7 +121,8 @@ class _UNetBFunction(torch.autograd.Function):
             k = P[n].numel()
             G[n] = flat[off:off + k].view(P[n].shape)
             off += k
-        ctx.eng.backward(ctx.ectx, P, G, list(g_heads))
+        ctx.eng.backward(ctx.ectx, P, G, list(g_heads), flat)
+        ctx.release.detach()
         ctx.ectx = None
         if parallel.is_initialized():
             parallel.allreduce_grads(flat)  # DataParallel reduce-add of replica gradients

@@ -1,0 +1,75 @@
+"""Launch-plan replay (engine.py): a replayed training step must compute what the recorded
+(Python-sequenced) step computes. Plans on vs off over several Adam steps; per-call outputs are
+not aliased across steps; a forward whose graph is dropped without backward frees its plan.
+
+Tolerance: the weight-gradient kernels accumulate with fp32 atomics (summation order varies run
+to run), so runs agree to fp32 rounding, not bit for bit: 1e-5 relative on losses and head
+outputs; parameters after three Adam steps within 5e-3 absolute (Adam normalises the update, so
+an element whose gradient is rounding noise moves by up to +-lr per step either way — the same
+bound the reference-parity tests use for later steps).
+"""
+import gc
+
+import numpy as np
+import pytest
+import torch
+
+import selectivenet_for_semantic_segmentation_binary_amd as S
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
+from tests.test_gpu_model import build
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(plans, steps=3, n=2, size=64, seed=0):
+    net = build(True, seed)
+    net._engine().plans_enabled = plans
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    loss_A = S.BCEWithLogitsLoss()
+    losses, outs = [], []
+    for s in range(steps):
+        x, lab = make_batch(n, size, seed=10 + s)
+        xt, lt = torch.tensor(x, device="cuda"), torch.tensor(lab, device="cuda")
+        o, sel, aux = net(xt)
+        loss = loss_A(aux, lt) + S.calc_selective_risk_image_b(o, sel, target=lt, lamb=2)[0]
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+        outs.append(o)  # held across steps: must keep this step's values
+    snap = [o.detach().cpu().numpy().copy() for o in outs]
+    params = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
+    return np.array(losses), snap, params, net
+
+
+def test_replayed_steps_match_recorded_steps():
+    l_on, o_on, p_on, net = _run(True)
+    l_off, o_off, p_off, _ = _run(False)
+    eng = net._engine()
+    assert sum(len(v) for v in eng._plans.values()) >= 1 and all(e.plan is not None for v in eng._plans.values()
+                                                                   for e in v)
+    assert np.allclose(l_on, l_off, rtol=1e-5, atol=0), (l_on, l_off)
+    for a, b in zip(o_on, o_off):
+        assert np.abs(a - b).max() <= 1e-4 * max(1.0, np.abs(b).max())
+    # outputs of different steps differ (no aliasing of a plan-owned buffer)
+    assert not np.array_equal(o_on[0], o_on[1])
+    for k in p_on:
+        assert np.abs(p_on[k] - p_off[k]).max() <= 5e-3, k
+
+
+def test_dropped_graph_releases_plan_and_eval_forward_replays():
+    net = build(True, 0)
+    eng = net._engine()
+    x, lab = make_batch(2, 32, seed=3)
+    xt = torch.tensor(x, device="cuda")
+    o, s, a = net(xt)  # training forward, graph kept...
+    entries = [e for v in eng._plans.values() for e in v]
+    assert len(entries) == 1 and entries[0].busy
+    del o, s, a  # ...then dropped without backward
+    gc.collect()
+    assert not entries[0].busy
+    net.eval()
+    with torch.no_grad():
+        r1 = net(xt)[0].clone()
+        r2 = net(xt)[0]  # replay of the eval plan
+    assert torch.equal(r1, r2)
