@@ -50,6 +50,15 @@ def synthetic_patchset(n: int, size: int = 256, seed: int = 0) -> PatchSet:
     return PatchSet(imgs, labs)
 
 
+def load_test_set_for_tests(spec: str, size: int, test_fold: int):
+    """The synthetic test fold `--data_dir synthetic:N` names: N patches, fold by index (uint8
+    images [N,H,W,3], labels [N,H,W])."""
+    n = int(spec.split(":")[1]) if ":" in spec else 64
+    imgs, labs = make_patches(5 * n, size, seed=1000)
+    idx = np.nonzero(np.arange(5 * n) % 5 + 1 == test_fold)[0]
+    return imgs[idx], labs[idx]
+
+
 # ----------------------------------------------------------------------------- split lists
 def _split_train_valid(rs, lst, valid_ratio=0.2):
     """utils/data_utils.py:52-56."""

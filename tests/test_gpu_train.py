@@ -145,3 +145,39 @@ def test_train_cli_epochs_checkpoints_resume(tmp_path):
     out2 = _cli(tmp_path, "--n_epoch", "1")
     assert "Load weights from" in out2 and "epoch 3 / 3" in out2
     assert sorted(os.listdir(ck))[-1] == "model_epoch3.pth"
+
+
+def test_eval_cli_matches_oracle_metrics(tmp_path):
+    """eval.py mirror on a checkpoint written by the train CLI: the device Evaluator's confusion
+    matrix equals the CPU oracle's eval-mode forward + the reference's fp32 sigmoid rule
+    (eval.py:175,179,233) + Evaluator (utils/compute_metric.py:10-26), up to pixels whose logit
+    lies within fp32 rounding of the cut (<= 1e-3 of the pixels)."""
+    _cli(tmp_path, "--n_epoch", "1")
+    ck = tmp_path / "1-fold" / "checkpoint"
+    out = tmp_path / "eval_out"
+    cmd = [sys.executable, "-m", "selectivenet_for_semantic_segmentation_binary_amd.eval", "--data_dir", "synthetic:8",
+           "--patch_size", "64", "--test_fold", "2", "--model_dir", str(ck), "--model_arch", "UNet_B",
+           "--selective", "1", "--select_eval", "1", "--batch_size", "4", "--save_dir", str(out)]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "mIoU:" in r.stdout and "rejection ratio:" in r.stdout
+    res = json.load(open(out / "performance.json"))
+
+    sd = torch.load(ck / "model_epoch1.pth", map_location="cpu", weights_only=True)["net"]
+    params, buffers = O.make_state(0, "RGB", True)
+    with torch.no_grad():
+        for k in params:
+            params[k].copy_(sd[k])
+        for k in buffers:
+            buffers[k].copy_(sd[k])
+    from selectivenet_for_semantic_segmentation_binary_amd.data import load_test_set_for_tests
+    imgs, labs = load_test_set_for_tests("synthetic:8", 64, 2)
+    x, lab = preprocess(imgs, labs)
+    with torch.no_grad():
+        o, s, _ = O.forward(params, buffers, torch.tensor(x), True, training=False)
+    pred = O.eval_pred_mask(o.numpy())
+    sel = O.eval_pred_mask(s.numpy())
+    cm = O.confusion_matrix(lab.astype("uint8"), pred, selection=sel)
+    got = np.array(res["confusion_matrix"])
+    assert np.abs(got - cm).sum() <= 1e-3 * lab.size, (got, cm)
+    assert abs(res["rejection_ratio"] - (1 - sel.mean())) <= 1e-3
