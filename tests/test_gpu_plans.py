@@ -2,11 +2,14 @@
 (Python-sequenced) step computes. Plans on vs off over several Adam steps; per-call outputs are
 not aliased across steps; a forward whose graph is dropped without backward frees its plan.
 
-Tolerance: the weight-gradient kernels accumulate with fp32 atomics (summation order varies run
-to run), so runs agree to fp32 rounding, not bit for bit: 1e-5 relative on losses and head
-outputs; parameters after three Adam steps within 5e-3 absolute (Adam normalises the update, so
-an element whose gradient is rounding noise moves by up to +-lr per step either way — the same
-bound the reference-parity tests use for later steps).
+Tolerance: the forward (convs, deterministic two-level BN reductions, heads) is bit-reproducible,
+so with frozen weights (lr=0) a replayed forward must equal the recorded one bit for bit. The
+weight-gradient kernels accumulate with fp32 atomics (summation order varies run to run), so
+over real Adam steps runs agree to fp32 rounding, not bit for bit: step-0 head outputs 1e-4
+relative (nothing has been updated yet); later steps' outputs 1e-2 relative to the tensor max and
+parameters within 5e-3 absolute (Adam normalises the update, so an element whose gradient is
+rounding noise moves by up to +-lr per step either way — the same bound the reference-parity
+tests use for later steps).
 """
 import gc
 
@@ -21,14 +24,14 @@ from tests.test_gpu_model import build
 pytestmark = pytest.mark.gpu
 
 
-def _run(plans, steps=3, n=2, size=64, seed=0):
+def _run(plans, steps=3, n=2, size=64, seed=0, lr=1e-3, same_batch=False):
     net = build(True, seed)
     net._engine().plans_enabled = plans
-    opt = S.Adam(net.parameters(), lr=1e-3)
+    opt = S.Adam(net.parameters(), lr=lr)
     loss_A = S.BCEWithLogitsLoss()
     losses, outs = [], []
     for s in range(steps):
-        x, lab = make_batch(n, size, seed=10 + s)
+        x, lab = make_batch(n, size, seed=10 + (0 if same_batch else s))
         xt, lt = torch.tensor(x, device="cuda"), torch.tensor(lab, device="cuda")
         o, sel, aux = net(xt)
         loss = loss_A(aux, lt) + S.calc_selective_risk_image_b(o, sel, target=lt, lamb=2)[0]
@@ -49,12 +52,23 @@ def test_replayed_steps_match_recorded_steps():
     assert sum(len(v) for v in eng._plans.values()) >= 1 and all(e.plan is not None for v in eng._plans.values()
                                                                    for e in v)
     assert np.allclose(l_on, l_off, rtol=1e-5, atol=0), (l_on, l_off)
-    for a, b in zip(o_on, o_off):
-        assert np.abs(a - b).max() <= 1e-4 * max(1.0, np.abs(b).max())
+    assert np.abs(o_on[0] - o_off[0]).max() <= 1e-4 * max(1.0, np.abs(o_off[0]).max())
+    for a, b in zip(o_on[1:], o_off[1:]):
+        assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
     # outputs of different steps differ (no aliasing of a plan-owned buffer)
     assert not np.array_equal(o_on[0], o_on[1])
     for k in p_on:
         assert np.abs(p_on[k] - p_off[k]).max() <= 5e-3, k
+
+
+def test_replay_with_frozen_weights_is_bit_exact():
+    # lr=0: parameters never move, the batch repeats, so step 0 (recorded) and steps 1-2
+    # (replayed) run the same forward on the same inputs and must agree bit for bit.
+    l_on, o_on, _, net = _run(True, lr=0.0, same_batch=True)
+    assert all(e.plan is not None for v in net._engine()._plans.values() for e in v)
+    for o in o_on[1:]:
+        assert np.array_equal(o, o_on[0])
+    assert l_on[1] == l_on[0] and l_on[2] == l_on[0]
 
 
 def test_dropped_graph_releases_plan_and_eval_forward_replays():
