@@ -144,21 +144,26 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
+    // all fragments of the step are read up front (16 B per lane each, 4*(MT+NT) reads), so the
+    // MFMAs of k-slice q overlap the LDS latency of slices q+1..3 instead of waiting per slice
+    uint4 af[4][MT], bfr[4][NT];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int boff = q * 32 + half * 16;
-      uint4 af[MT], bfr[NT];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
-        af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
+        af[q][a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
 #pragma unroll
       for (int b = 0; b < NT; ++b)
-        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+        bfr[q][b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler would sink them)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
-        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
-    }
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[q][a], bfr[q][b]);
   };
 
   // ---------------------------------------------------------------- prologue: chunk 0, B(0), B(1)
@@ -435,16 +440,29 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
       s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow + 4][pcol]);
       const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       const int xcol = wj * 32 + 16 * grp_hi + 4 * p4;
+      // tap fragments are read PF taps ahead of their MFMA (a rolling window of PF+1 fragments:
+      // hoisting all nine would spill), pinned in that order with sched_group_barrier so the LDS
+      // latency hides behind the MFMAs already issued instead of being waited out per MFMA
+      constexpr int PF = 3;
+      auto read_tap = [&](int t) __attribute__((always_inline)) {
+        const int tap = min(tap0 + t, 8);
+        const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+        const int xrow = (ks + dy) * WHW + 8 * half + dx + q4;
+        s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow][xcol]);
+        s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow + 4][xcol]);
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      bf16x8 bfr[NTAP];
+#pragma unroll
+      for (int t = 0; t < PF && t < NTAP; ++t) bfr[t] = read_tap(t);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * PF, 0);
 #pragma unroll
       for (int t = 0; t < NTAP; ++t) {
-        if (t < ntap) {
-          const int tap = tap0 + t;
-          const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-          const int xrow = (ks + dy) * WHW + 8 * half + dx + q4;
-          s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow][xcol]);
-          s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow + 4][xcol]);
-          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[t], 0, 0, 0);
+        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[t], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (t + PF < NTAP) {
+          bfr[t + PF] = read_tap(t + PF);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         }
       }
     }
