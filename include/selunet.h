@@ -125,9 +125,14 @@ int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float
  * data-gradient, conv_transpose2d forward and data-gradient (model.py:11,44,51,57). */
 int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
                         const selunet_epilogue* ep, int32_t dtype, void* stream);
-/* Rows of the stats slab selunet_gemm_gather writes for this operand (pixel tiles of the
- * kernel it dispatches to: 16x16 halo tiles for 3x3 taps, else 128-row tiles); -1 on error. */
+/* Rows of the stats slab selunet_gemm_gather writes for this operand (workgroup rows of the
+ * kernel it dispatches to: 16x16 halo tiles for single-chunk 3x3 operands, the persistent
+ * workgroups of the multi-chunk halo kernel, else 128-row tiles); -1 on error. */
 int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t dtype);
+/* Tuning/testing knob: workgroups the persistent multi-chunk 3x3 kernel targets (default 256, one
+ * per MI355X CU; wgs <= 0 restores the default). Returns the previous value. The stats-slab row
+ * count depends on it: query selunet_gemm_stats_rows after changing it. Not thread-safe. */
+int32_t selunet_set_halo_workgroups(int32_t wgs);
 /* Name of the kernel a selunet_gemm_gather (q == NULL; mode = epilogue mode) or
  * selunet_gemm_wgrad (q = the Q operand) call with these operands dispatches to. */
 const char* selunet_gemm_kernel_name(const selunet_gather* a, const selunet_gather* q, int32_t n_cols,

@@ -144,26 +144,21 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
     const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
-    // all fragments of the step are read up front (16 B per lane each, 4*(MT+NT) reads), so the
-    // MFMAs of k-slice q overlap the LDS latency of slices q+1..3 instead of waiting per slice
-    uint4 af[4][MT], bfr[4][NT];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int boff = q * 32 + half * 16;
+      uint4 af[MT], bfr[NT];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
-        af[q][a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
+        af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
 #pragma unroll
       for (int b = 0; b < NT; ++b)
-        bfr[q][b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler would sink them)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
+        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
-        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[q][a], bfr[q][b]);
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+    }
   };
 
   // ---------------------------------------------------------------- prologue: chunk 0, B(0), B(1)
@@ -275,6 +270,274 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
   };
   auto bias_col = [&](int c) { return n0 + c; };
   lds_tile_store<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, ptile, n0, N));
+}
+
+// =========================================================================== persistent variant
+// Multi-chunk layers (C > one chunk) at one workgroup per CU: a non-persistent workgroup exposes
+// its prologue (first halo chunk and weights from HBM, nothing else resident to overlap it) and its
+// epilogue on every tile. Here each workgroup keeps one column tile (n0) and walks the output tiles
+// prow, prow + gp, prow + 2 gp, ...; its (tile, chunk) jobs form one stream, so the first chunk of
+// tile i+1 and its weights are loaded during the last chunk of tile i. Those loads stay in registers
+// until the epilogue of tile i (which uses the whole LDS) is done, then go to LDS. The epilogue's
+// column sums (BN statistics / colsum / BN-backward sums) accumulate in registers over the tiles
+// and are reduced once: one slab row per workgroup (row prow, see conv3x3_halo_stats_rows).
+template <typename T, int BN>
+__global__ void __launch_bounds__(HTHREADS, 1)
+conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles,
+                            int tiles_x, int tiles_y, int ptiles, int gp) {
+  constexpr int E = 16 / sizeof(T);
+  constexpr int CK = 128 / sizeof(T);
+  constexpr int WAVES_N = BN / 64;
+  constexpr int WAVES_M = 8 / WAVES_N;
+  constexpr int WPIX = (TH * TW) / WAVES_M;
+  constexpr int MT = WPIX / 32;
+  constexpr int NT = 2;
+  constexpr int B_ROUNDS = BN * 8 / HTHREADS;
+  static_assert(B_ROUNDS * HTHREADS == BN * 8, "weight tile rows must split evenly over the threads");
+  constexpr int AD = 3;
+  static_assert(AD + A_ROUNDS <= 9, "halo slices must be written within the chunk's nine taps");
+
+  constexpr int SMEM_MAIN = 2 * HPIX * AROWB + 2 * BN * ROWB + 2 * CK * 8;
+  constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + 2 * HPIX * AROWB;
+  float* Ss = reinterpret_cast<float*>(Bs + 2 * BN * ROWB);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n_tile = lb % n_tiles;
+  const int prow = lb / n_tiles;
+  const int n0 = n_tile * BN;
+  const int ntl = prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0;  // host: gp <= ptiles, so >= 1
+  const int nchunks = g.Ctot / CK;
+  const int csteps = nchunks * 9;  // steps per tile
+
+  auto tile_xy = [&](int i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned pt = (unsigned)(prow + i * gp);
+    const unsigned r = pt / (unsigned)tiles_x;
+    x0 = (int)(pt - r * (unsigned)tiles_x) * TW;
+    const unsigned r2 = r / (unsigned)tiles_y;
+    y0 = (int)(r - r2 * (unsigned)tiles_y) * TH;
+    img = (int)r2;
+  };
+  auto a_slot = [&](int round, int& hp, int& cc) -> bool {
+    const int hidx = round * HTHREADS + tid;
+    hp = min(hidx >> 3, HPIX - 1);
+    cc = hidx & 7;
+    return hidx < HPIX * 8;
+  };
+  auto a_inside = [&](int y0, int x0, int hp) -> bool {
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    return (unsigned)(y0 - 1 + hy) < (unsigned)g.h && (unsigned)(x0 - 1 + hx) < (unsigned)g.w;
+  };
+  // source (and its channel base) of chunk `chunk`; a chunk never straddles sources
+  auto chunk_src = [&](int chunk, int& c) -> SrcArg {
+    c = chunk * CK;
+    const bool s1 = g.nsrc > 1 && c >= g.src[0].C;
+    if (s1) c -= g.src[0].C;
+    return pick_src(g, s1 ? 1 : 0);
+  };
+  auto a_ptr = [&](const SrcArg& sa, int c, int img, int y0, int x0, int hp, int cc) -> const uint4* {
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    const int ys = min(max(y0 - 1 + hy, 0), g.h - 1), xs = min(max(x0 - 1 + hx, 0), g.w - 1);
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
+                                          (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + c + cc * E);
+  };
+  struct BRegs {
+    uint4 v[B_ROUNDS];
+  };
+  auto b_load = [&](int st) __attribute__((always_inline)) {  // st: step within a tile
+    const int chunk = st / 9, tap = st - chunk * 9;
+    const int k0 = tap * g.Ctot + chunk * CK;
+    BRegs rb;
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      rb.v[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
+    }
+    return rb;
+  };
+  auto b_store = [&](const BRegs& rb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb.v[r];
+    }
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+  int hrow0[MT], hsw0[MT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+    const int pix = wm * WPIX + a * 32 + l32;
+    hrow0[a] = (pix / TW) * HWT + (pix % TW);
+    hsw0[a] = half ^ ((pix / TW) & 1);
+  }
+  auto mma_step = [&](int hbuf, int bbuf, int t) __attribute__((always_inline)) {
+    const unsigned char* a_src = As + hbuf * HPIX * AROWB;
+    const unsigned char* b_src = Bs + bbuf * BN * ROWB;
+    const int dy = t / 3, dx = t - (t / 3) * 3;
+    const int tap_off = dy * HWT + dx;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int boff = q * 32 + half * 16;
+      uint4 af[MT], bfr[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+        af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+    }
+  };
+  // write halo slice `r` (raw registers v) of chunk source sa/c of the tile at (y0, x0) to buffer
+  // hb, transformed with the global coefficients (used outside the steady-state loop)
+  auto halo_put_global = [&](uint4 v, int r, const SrcArg& sa, int c, int y0, int x0, int hb)
+      __attribute__((always_inline)) {
+    int hp, cc;
+    if (!a_slot(r, hp, cc)) return;
+    uint4 o = make_uint4(0, 0, 0, 0);
+    if (a_inside(y0, x0, hp)) o = sa.scale ? transform16<T>(v, sa.scale, sa.shift, c + cc * E, sa.relu) : v;
+    *reinterpret_cast<uint4*>(As + hb * HPIX * AROWB + halo_off(hp, cc)) = o;
+  };
+
+  // ---------------------------------------------------------------- prologue: tile 0 chunk 0, B(0), B(1)
+  {
+    int img, y0, x0;
+    tile_xy(0, img, y0, x0);
+    int c0;
+    const SrcArg sa = chunk_src(0, c0);
+    uint4 v0[A_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) {
+      int hp, cc;
+      a_slot(r, hp, cc);
+      v0[r] = *a_ptr(sa, c0, img, y0, x0, hp, cc);
+    }
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) halo_put_global(v0[r], r, sa, c0, y0, x0, 0);
+  }
+  BRegs rb_next = b_load(0);
+  b_store(rb_next, 0);
+  rb_next = b_load(1 % csteps);
+  __syncthreads();
+
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const TileStats ts = tile_stats(ep, prow, n0, N);
+  float* tile = reinterpret_cast<float*>(smem);  // epilogue: [256][BN + 4] over the whole LDS
+  uint4 ra[A_ROUNDS];
+  int J = 0;  // job (tile, chunk) counter: halo buffer J & 1
+  int S = 0;  // step counter: weight buffer S & 1
+  for (int i = 0; i < ntl; ++i) {
+    int img, y0, x0;
+    tile_xy(i, img, y0, x0);
+    BRegs rb_hold;
+    for (int c = 0; c < nchunks; ++c, ++J) {
+      const bool last_c = c + 1 == nchunks;
+      const bool has_next = !last_c || i + 1 < ntl;
+      const bool defer = last_c && has_next;  // next job is the next tile: LDS writes after the epilogue
+      int nimg = img, ny0 = y0, nx0 = x0;
+      if (defer) tile_xy(i + 1, nimg, ny0, nx0);
+      const int nc = !has_next ? c : (last_c ? 0 : c + 1);
+      int cs;
+      const SrcArg sn = chunk_src(nc, cs);
+      float* ssc = Ss + ((J + 1) & 1) * CK;
+      float* ssh = Ss + 2 * CK + ((J + 1) & 1) * CK;
+      float coef = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int st2 = c * 9 + t + 2;
+        const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);  // next tile's steps wrap
+        if (t == 0 && !defer && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
+        if (t < A_ROUNDS) {
+          int hp, cc;
+          a_slot(t, hp, cc);
+          ra[t] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
+        }
+        mma_step(J & 1, S & 1, t);
+        if (defer && t == 8) rb_hold = rb_next;  // B(S + 1): stored after the epilogue
+        else b_store(rb_next, (S + 1) & 1);
+        if (!defer) {
+          if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
+          if (t >= AD && t - AD < A_ROUNDS) {
+            const int r = t - AD;
+            int hp, cc;
+            if (a_slot(r, hp, cc)) {
+              uint4 v = make_uint4(0, 0, 0, 0);
+              if (a_inside(ny0, nx0, hp)) {
+                v = ra[r];
+                if (sn.scale) {
+                  T e[E];
+                  __builtin_memcpy(e, &v, 16);
+#pragma unroll
+                  for (int j = 0; j < E; ++j) {
+                    float f = to_f(e[j]) * ssc[cc * E + j] + ssh[cc * E + j];
+                    if (sn.relu) f = fmaxf(f, 0.0f);
+                    e[j] = from_f<T>(f);
+                  }
+                  __builtin_memcpy(&v, e, 16);
+                }
+              }
+              *reinterpret_cast<uint4*>(As + ((J + 1) & 1) * HPIX * AROWB + halo_off(hp, cc)) = v;
+            }
+          }
+        }
+        __syncthreads();
+        rb_next = rb_far;
+        ++S;
+      }
+      if (defer) {
+        // (kept for after the epilogue: ra[] = next tile's chunk 0, rb_hold = B(S), rb_next = B(S+1))
+      }
+    }
+
+    // ------------------------------------------------------------ epilogue of tile i
+    acc_to_lds<MT, NT, BN>(tile, acc, wm * WPIX, wn * 64, lane);
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+    __syncthreads();
+    auto dst = [&](int pix, int cl) -> T* {
+      const int y = y0 + pix / TW, x = x0 + pix % TW;
+      if (y >= g.h || x >= g.w) return nullptr;
+      const int64_t m = ((int64_t)img * g.h + y) * g.w + x;
+      const int col = n0 + cl;
+      if (ep.mode == SELUNET_EP_SPLIT)
+        return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                              : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+      return reinterpret_cast<T*>(ep.out0) + m * N + col;
+    };
+    auto bias_col = [&](int cl) { return n0 + cl; };
+    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+    if (i + 1 < ntl) {
+      __syncthreads();  // the tile has been read: LDS back to halo / weights
+      int nimg, ny0, nx0;
+      tile_xy(i + 1, nimg, ny0, nx0);
+      int cs;
+      const SrcArg sn = chunk_src(0, cs);
+#pragma unroll
+      for (int r = 0; r < A_ROUNDS; ++r) halo_put_global(ra[r], r, sn, cs, ny0, nx0, J & 1);
+      b_store(rb_hold, S & 1);
+      __syncthreads();
+    }
+  }
+  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3);
 }
 
 // =========================================================================== weight gradient
@@ -527,12 +790,49 @@ int64_t conv3x3_halo_tiles(const GatherArg& g) {
   return (int64_t)g.n * cdiv(g.h, TH) * cdiv(g.w, TW);
 }
 
+// Workgroups (= CUs) the persistent multi-chunk kernel targets; a fixed constant rather than the
+// device's CU count so that the statistics slab rows the host allocates never depend on the device.
+constexpr int PERSIST_WGS_DEFAULT = 256;
+static int PERSIST_WGS = PERSIST_WGS_DEFAULT;  // selunet_set_halo_workgroups
+
+static bool persist_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("SELUNET_HALO_PERSIST");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+static bool halo_one_chunk(const GatherArg& g, int dtype) { return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64); }
+
+// output tiles per workgroup row of the persistent launch (= statistics slab rows): PERSIST_WGS
+// workgroups at 128-column tiles; 64-column tiles (N % 128 != 0 or a split at 64) use twice the
+// workgroups with the same rows, so the row count depends on the operand and N only
+static int persist_rows(const GatherArg& g, int N) {
+  const int64_t pt = conv3x3_halo_tiles(g);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(pt, PERSIST_WGS / std::max(1, N / 128)));
+}
+
+bool conv3x3_halo_persistent(const GatherArg& g, int dtype) { return !halo_one_chunk(g, dtype) && persist_enabled(); }
+
+int64_t conv3x3_halo_stats_rows(const GatherArg& g, int N, int dtype) {
+  if (halo_one_chunk(g, dtype) || !persist_enabled()) return conv3x3_halo_tiles(g);
+  return persist_rows(g, N);
+}
+
 template <typename T, int BN>
 static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
   const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
   const int n_tiles = N / BN;
   const int64_t blocks = conv3x3_halo_tiles(g) * n_tiles;
   const bool one = g.Ctot == 128 / (int)sizeof(T);
+  if (!one && persist_enabled()) {
+    const int gp = persist_rows(g, N);
+    hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g,
+                       reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
+                       (int)conv3x3_halo_tiles(g), gp);
+    return;
+  }
   auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N, k_pad,
                      ep, n_tiles, tiles_x, tiles_y);
@@ -554,3 +854,9 @@ int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, con
 }
 
 }  // namespace selunet
+
+extern "C" int32_t selunet_set_halo_workgroups(int32_t wgs) {
+  const int prev = selunet::PERSIST_WGS;
+  selunet::PERSIST_WGS = wgs > 0 ? wgs : selunet::PERSIST_WGS_DEFAULT;
+  return prev;
+}

@@ -627,7 +627,7 @@ extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_co
   const int esz = dtype == SELUNET_F32 ? 4 : 2;
   GatherArg g;
   if (make_gather(a, dtype, g, 16 / esz)) return -1;
-  if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_tiles(g);
+  if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_stats_rows(g, n_cols, dtype);
   return cdiv(g.M, BM);
 }
 
@@ -645,6 +645,9 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
       const bool one = g.Ctot == (bf ? 64 : 32);  // single channel chunk: 64-column tiles, 2 WG/CU
       const bool bn128 = !one && n_cols % 128 == 0 && !(mode == SELUNET_EP_SPLIT && (n_cols / 2) % 128 != 0);
       if (one) return bf ? "conv3x3_halo1<bf16,64>" : "conv3x3_halo1<f32,64>";
+      if (conv3x3_halo_persistent(g, dtype))
+        return bf ? (bn128 ? "conv3x3_halo_persist<bf16,128>" : "conv3x3_halo_persist<bf16,64>")
+                  : (bn128 ? "conv3x3_halo_persist<f32,128>" : "conv3x3_halo_persist<f32,64>");
       return bf ? (bn128 ? "conv3x3_halo<bf16,128>" : "conv3x3_halo<bf16,64>")
                 : (bn128 ? "conv3x3_halo<f32,128>" : "conv3x3_halo<f32,64>");
     }

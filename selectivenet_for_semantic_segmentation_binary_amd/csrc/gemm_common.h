@@ -240,9 +240,13 @@ __device__ __forceinline__ TileStats tile_stats(const EpiArg& ep, int64_t row, i
 // Store the LDS tile as 8-column vectors (16 B bf16 / 32 B fp32): dst(row, col) returns the
 // global address of tile element (row, col) (col a multiple of 8) or nullptr for a masked row.
 // bias (nullable) is indexed by bias_col(col).
+// The statistics are accumulated into the thread's s1/s2/s3 (8 columns each: the thread's column
+// chunk is tid % (TC / 8) for every tile, so a persistent workgroup can accumulate over its tiles)
+// and reduced across the workgroup by tile_stats_flush.
 template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
-__device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
-                                               const TileStats& ts) {
+__device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& dst, const float* bias,
+                                                   BiasCol&& bias_col, const TileStats& ts, float (&s1)[8],
+                                                   float (&s2)[8], float (&s3)[8]) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass
   const int cc = tid % CC, r0 = tid / CC;
@@ -263,7 +267,6 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
       is[e] = ts.bnb.invstd[col + e];
     }
   }
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
@@ -316,10 +319,22 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
       }
     }
   }
+}
+
+// Reduce the s1/s2/s3 accumulators of lds_tile_store_acc over the workgroup (LDS scratch `red`,
+// RS * TC * 3 floats; the caller has finished with whatever `red` held) and write the slab row.
+template <int TC, int NTHREADS>
+__device__ __forceinline__ void tile_stats_flush(float* red, int tid, const TileStats& ts, const float (&s1)[8],
+                                                 const float (&s2)[8], const float (&s3)[8]) {
+  constexpr int CC = TC / 8;
+  constexpr int RS = NTHREADS / CC;
+  const int cc = tid % CC, r0 = tid / CC;
+  const int col = cc * 8;
+  const bool do_st = ts.stats != nullptr;
+  const bool do_bn = ts.bnb.slab != nullptr;
   const int nst = do_bn ? 3 : (do_st ? 2 : 1);
   if (do_st || ts.colsum != nullptr || do_bn) {
     __syncthreads();  // everyone is done reading the tile: reuse it for the column reduction
-    float* red = tile;  // [RS][TC][3]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       red[(r0 * TC + col + e) * 3 + 0] = s1[e];
@@ -338,6 +353,14 @@ __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, 
   }
 }
 
+template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
+__device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
+                                               const TileStats& ts) {
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  lds_tile_store_acc<T, TR, TC, NTHREADS>(tile, tid, dst, bias, bias_col, ts, s1, s2, s3);
+  tile_stats_flush<TC, NTHREADS>(tile, tid, ts, s1, s2, s3);
+}
+
 // host: validate a C-ABI gather descriptor and convert it (gemm.hip)
 int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems);
 
@@ -345,6 +368,8 @@ int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems)
 // false when the operand is not eligible (caller falls back to the generic gather GEMM).
 bool conv3x3_halo_eligible(const GatherArg& g, int N, int dtype);
 int64_t conv3x3_halo_tiles(const GatherArg& g);
+int64_t conv3x3_halo_stats_rows(const GatherArg& g, int N, int dtype);  // slab rows of the halo epilogue
+bool conv3x3_halo_persistent(const GatherArg& g, int dtype);            // multi-chunk: persistent kernel
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);

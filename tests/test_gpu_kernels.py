@@ -30,6 +30,19 @@ def nchw(t, n, h, w):
     return t.reshape(n, h, w, -1).permute(0, 3, 1, 2)
 
 
+@pytest.fixture
+def halo_wgs():
+    """Set the persistent halo kernel's workgroup target for one test (0 = default), restored after."""
+    prev = []
+
+    def set_(wgs):
+        prev.append(K.query("selunet_set_halo_workgroups", wgs))
+
+    yield set_
+    if prev:
+        K.query("selunet_set_halo_workgroups", prev[0])
+
+
 def gen(*shape, seed=0, scale=1.0):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(*shape, generator=g) * scale
@@ -62,7 +75,11 @@ def pack(w, dt=torch.float32):
     (64, 64, 128, 1, 16, 48, True),    # halo kernel, two sources, BN = 128
     (128, 0, 256, 2, 20, 24, True),    # halo kernel, partial edge tiles
 ])
-def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform):
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
+    """wgs = 3: the persistent multi-chunk halo kernel with 3 workgroup rows, so every workgroup
+    walks several (unevenly many) tiles and accumulates its statistics over them."""
+    halo_wgs(wgs)
     x0 = gen(n, cin0, h, w, seed=1)
     x1 = gen(n, cin1, h, w, seed=2) if cin1 else None
     wt = gen(cout, cin0 + cin1, 3, 3, seed=3, scale=0.05)
@@ -113,7 +130,9 @@ def test_conv3x3_fwd_small_c_nchw():
 @pytest.mark.parametrize("cin,cout,split,h,w", [(64, 64, 0, 8, 8), (128, 64, 64, 8, 8), (512, 256, 256, 8, 8),
                                                 (64, 128, 0, 8, 8), (64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
                                                 (256, 128, 128, 16, 48)])
-def test_conv3x3_dgrad(cin, cout, split, h, w):
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_conv3x3_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+    halo_wgs(wgs)
     n = 2
     wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
     dy = gen(n, cout, h, w, seed=7)
@@ -342,9 +361,11 @@ def _bf(t):
 @pytest.mark.parametrize("cin0,cin1,cout,small,h,w", [(64, 0, 64, False, 16, 16), (64, 64, 128, False, 16, 16),
                                                       (256, 0, 512, False, 16, 16), (3, 0, 64, True, 16, 16),
                                                       (128, 0, 64, False, 20, 40), (64, 128, 64, False, 24, 17)])
-def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small, h, w):
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small, h, w, wgs, halo_wgs):
     """bf16 operands, fp32 accumulation: compared with fp32 torch on the same bf16-rounded data
     (sizes >= 16 take the halo-tiled kernels, incl. partial edge tiles)."""
+    halo_wgs(wgs)
     n = 2
     x0 = _bf(gen(n, cin0, h, w, seed=40))
     x1 = _bf(gen(n, cin1, h, w, seed=41)) if cin1 else None

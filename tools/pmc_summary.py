@@ -16,6 +16,10 @@ from collections import defaultdict
 
 # rocprofv3 kernel-name pattern -> selunet kernel name
 NAME_MAP = [
+    (r"conv3x3_halo_persist_kernelIDF16bLi128", "conv3x3_halo_persist<bf16,128>"),
+    (r"conv3x3_halo_persist_kernelIDF16bLi64", "conv3x3_halo_persist<bf16,64>"),
+    (r"conv3x3_halo_persist_kernelIfLi128", "conv3x3_halo_persist<f32,128>"),
+    (r"conv3x3_halo_persist_kernelIfLi64", "conv3x3_halo_persist<f32,64>"),
     (r"conv3x3_halo_kernelIDF16bLi64ELb1", "conv3x3_halo1<bf16,64>"),
     (r"conv3x3_halo_kernelIfLi64ELb1", "conv3x3_halo1<f32,64>"),
     (r"conv3x3_halo_kernelIDF16bLi128", "conv3x3_halo<bf16,128>"),
