@@ -15,6 +15,14 @@
 
 #include "gemm_common.h"
 
+// SELUNET_ABL: timing ablations of the persistent kernel (tools/ablate.sh; results are WRONG for
+// any value but 0), a bit mask: 1 fragment reads hoisted, 2 no weight staging, 4 no halo
+// prefetch, 8 one barrier per chunk instead of per tap, 16 no MFMAs, 32 no epilogue stores,
+// 64 no fragment reads (constant operands).
+#ifndef SELUNET_ABL
+#define SELUNET_ABL 0
+#endif
+
 namespace selunet {
 
 constexpr int TH = 16, TW = 16;         // output tile (pixels)
@@ -294,8 +302,11 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   constexpr int NT = 2;
   constexpr int B_ROUNDS = BN * 8 / HTHREADS;
   static_assert(B_ROUNDS * HTHREADS == BN * 8, "weight tile rows must split evenly over the threads");
-  constexpr int AD = 3;
-  static_assert(AD + A_ROUNDS <= 9, "halo slices must be written within the chunk's nine taps");
+  // tap at which halo slice r of the next job is loaded / written to LDS (written at >= 2: the
+  // coefficients staged at tap 1 are visible from tap 2 on)
+  auto halo_load_tap = [](int r) { return r; };
+  auto halo_write_tap = [](int r) { return r + 3; };
+  static_assert(A_ROUNDS <= 6, "halo slice schedule covers six slices");
 
   constexpr int SMEM_MAIN = 2 * HPIX * AROWB + 2 * BN * ROWB + 2 * CK * 8;
   constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
@@ -389,21 +400,48 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
+#if (SELUNET_ABL & 1)
+    uint4 af[4][MT], bfr[4][NT];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int boff = q * 32 + half * 16;
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+        af[q][a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bfr[q][b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[q][a], bfr[q][b]);
+#else
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int boff = q * 32 + half * 16;
       uint4 af[MT], bfr[NT];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
-        af[a] = *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
+        af[a] = (SELUNET_ABL & 64) ? make_uint4(q, a, t, 1)
+                                   : *reinterpret_cast<const uint4*>(a_src + (hrow0[a] + tap_off) * AROWB + q * 32 + ((hsw0[a] ^ dy) & 1) * 16);
 #pragma unroll
       for (int b = 0; b < NT; ++b)
-        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+        bfr[b] = (SELUNET_ABL & 64) ? make_uint4(q, b, t, 2)
+                                    : *reinterpret_cast<const uint4*>(b_src + (wn * 64 + b * 32 + l32) * ROWB + boff);
+#if (SELUNET_ABL & 16)
+      asm volatile("" :: "v"(af[0].x ^ af[MT - 1].w), "v"(bfr[0].x ^ bfr[NT - 1].w));
+#else
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+#endif
     }
+#endif
   };
   // write halo slice `r` (raw registers v) of chunk source sa/c of the tile at (y0, x0) to buffer
   // hb, transformed with the global coefficients (used outside the steady-state loop)
@@ -461,21 +499,29 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       float coef = 0.0f;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int st2 = c * 9 + t + 2;
+        const int st2 = c * 9 + t + 2;  // weights are loaded two steps ahead
+#if (SELUNET_ABL & 2)
+        const BRegs rb_far = rb_next;
+#else
         const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);  // next tile's steps wrap
+#endif
         if (t == 0 && !defer && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
-        if (t < A_ROUNDS) {
-          int hp, cc;
-          a_slot(t, hp, cc);
-          ra[t] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
+#pragma unroll
+        for (int r = 0; r < A_ROUNDS; ++r) {
+          if (!(SELUNET_ABL & 4) && halo_load_tap(r) == t) {
+            int hp, cc;
+            a_slot(r, hp, cc);
+            ra[r] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
+          }
         }
         mma_step(J & 1, S & 1, t);
         if (defer && t == 8) rb_hold = rb_next;  // B(S + 1): stored after the epilogue
-        else b_store(rb_next, (S + 1) & 1);
+        else if (!(SELUNET_ABL & 2)) b_store(rb_next, (S + 1) & 1);
         if (!defer) {
           if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
-          if (t >= AD && t - AD < A_ROUNDS) {
-            const int r = t - AD;
+#pragma unroll
+          for (int r = 0; r < A_ROUNDS; ++r) {
+            if ((SELUNET_ABL & 4) || halo_write_tap(r) != t) continue;
             int hp, cc;
             if (a_slot(r, hp, cc)) {
               uint4 v = make_uint4(0, 0, 0, 0);
@@ -497,7 +543,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
             }
           }
         }
-        __syncthreads();
+        if (!(SELUNET_ABL & 8) || t == 8) __syncthreads();
         rb_next = rb_far;
         ++S;
       }
@@ -524,7 +570,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       return reinterpret_cast<T*>(ep.out0) + m * N + col;
     };
     auto bias_col = [&](int cl) { return n0 + cl; };
-    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+    if (!(SELUNET_ABL & 32)) lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
     if (i + 1 < ntl) {
       __syncthreads();  // the tile has been read: LDS back to halo / weights
       int nimg, ny0, nx0;
@@ -827,7 +873,8 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   const int64_t blocks = conv3x3_halo_tiles(g) * n_tiles;
   const bool one = g.Ctot == 128 / (int)sizeof(T);
   if (!one && persist_enabled()) {
-    const int gp = persist_rows(g, N);
+    const int dtype = sizeof(T) == 2 ? SELUNET_BF16 : SELUNET_F32;
+    const int gp = (int)conv3x3_halo_stats_rows(g, N, dtype);
     hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g,
                        reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
                        (int)conv3x3_halo_tiles(g), gp);

@@ -249,6 +249,9 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
                                                    float (&s2)[8], float (&s3)[8]) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass
+  // an opaque copy of tid: in a persistent kernel the column coefficients below are invariant over
+  // its tile loop, and hoisting them out of it would pin ~40 VGPRs through the MFMA main loop
+  asm volatile("" : "+v"(tid));
   const int cc = tid % CC, r0 = tid / CC;
   const int col = cc * 8;
   float bv[8];

@@ -458,3 +458,83 @@ def test_first_conv_fwd_and_wgrad(dt, cin, n, h, w):
     gw = torch.empty(64, cin, 3, 3, device=DEV)
     K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), 64, cin, 32, K.ptr(gw), K.stream_ptr())
     assert rel(gw.cpu(), ref_w) < (TOL if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,n,h,w", [
+    (128, 0, 128, 2, 20, 72),    # partial tiles in both directions
+    (128, 128, 256, 1, 33, 40),  # two sources (torch.cat), two column tiles
+    (256, 0, 512, 2, 32, 32),    # four chunks, four column tiles
+])
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_conv3x3_bf16_persist_fwd_stats(cin0, cin1, cout, n, h, w, wgs, halo_wgs):
+    """bf16 multi-chunk 3x3 forward on the persistent halo kernel with the BN statistics epilogue;
+    wgs = 3 makes every workgroup walk several tiles."""
+    halo_wgs(wgs)
+    x0 = _bf(gen(n, cin0, h, w, seed=60))
+    x1 = _bf(gen(n, cin1, h, w, seed=61)) if cin1 else None
+    s0, t0 = bn_fold(cin0, 62)
+    wt = _bf(gen(cout, cin0 + cin1, 3, 3, seed=63, scale=0.05))
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    a = _bf(torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)))
+    keep = [d(nhwc(x0)).bfloat16(), d(s0), d(t0)]
+    srcs = [K.source(keep[0], cin0, keep[1], keep[2])]
+    if cin1:
+        a = torch.cat((a, x1), 1)
+        keep.append(d(nhwc(x1)).bfloat16())
+        srcs.append(K.source(keep[3], cin1))
+    ref = F.conv2d(a, wt, padding=1)
+    fwd, _, kpad = pack(wt, torch.bfloat16)
+    g = K.gather(n, h, w, 9, *srcs)
+    M = n * h * w
+    out = torch.empty(M, cout, dtype=torch.bfloat16, device=DEV)
+    rows = K.query("selunet_gemm_stats_rows", g, cout, K.BF16)
+    stats = torch.empty(rows, 2, cout, device=DEV)
+    ep = K.Epilogue(K.ptr(out), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+    K.call("selunet_gemm_gather", g, K.ptr(fwd), cout, kpad, ep, K.BF16, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel(nchw(out.float().cpu(), n, h, w), ref) < 1e-2
+    st = stats.cpu().double().sum(0)
+    r = ref.double().permute(1, 0, 2, 3).reshape(cout, -1)
+    assert rel(st[0], r.sum(1)) < 1e-3 and rel(st[1], (r * r).sum(1)) < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,split,h,w", [(256, 128, 0, 20, 40), (256, 128, 128, 16, 64),
+                                                (512, 256, 256, 32, 32)])
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_conv3x3_bf16_persist_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+    """bf16 data gradient on the persistent halo kernel: plain with the producer's BN-backward sums,
+    and the torch.cat split with the ConvTranspose2d bias column sums."""
+    halo_wgs(wgs)
+    n = 2
+    wt = _bf(gen(cout, cin, 3, 3, seed=64, scale=0.05))
+    dy = _bf(gen(n, cout, h, w, seed=65))
+    x = gen(n, cin, h, w, seed=66).requires_grad_()
+    (ref,) = torch.autograd.grad(F.conv2d(x, wt, padding=1), x, dy)
+    _, dg, _ = pack(wt, torch.bfloat16)
+    dyd = nhwc(dy).to(DEV).bfloat16()
+    M = n * h * w
+    g = K.gather(n, h, w, 9, K.source(dyd, cout))
+    rows = K.query("selunet_gemm_stats_rows", g, cin, K.BF16)
+    if split:
+        d0 = torch.empty(M, split, dtype=torch.bfloat16, device=DEV)
+        d1 = torch.empty(M, cin - split, dtype=torch.bfloat16, device=DEV)
+        colsum = torch.empty(rows, split, device=DEV)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split, K.ptr(colsum))
+        K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.BF16, K.stream_ptr())
+        torch.cuda.synchronize()
+        got = torch.cat((nchw(d0.float().cpu(), n, h, w), nchw(d1.float().cpu(), n, h, w)), 1)
+        assert rel(colsum.double().sum(0).cpu(), d0.double().sum(0).cpu()) < 1e-5
+    else:
+        dx = torch.empty(M, cin, dtype=torch.bfloat16, device=DEV)
+        yprev = gen(M, cin, seed=67).to(DEV).bfloat16()
+        sc, sh = (gen(cin, seed=68).abs() + 0.5).to(DEV), (gen(cin, seed=69) * 0.3).to(DEV)
+        mean, invstd = (gen(cin, seed=70) * 0.1).to(DEV), (gen(cin, seed=71).abs() + 0.5).to(DEV)
+        slab = torch.empty(rows, 3, cin, device=DEV)
+        ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+        ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+        K.call("selunet_gemm_gather", g, K.ptr(dg), cin, 9 * cout, ep, K.BF16, K.stream_ptr())
+        torch.cuda.synchronize()
+        got = nchw(dx.float().cpu(), n, h, w)
+        check_bnb_sums(slab.cpu(), dx.float().cpu(), yprev.float().cpu(), sc.cpu(), sh.cpu(), mean.cpu(),
+                       invstd.cpu(), tol=1e-4)
+    assert rel(got, ref) < 1e-2
