@@ -74,6 +74,7 @@ def pack(w, dt=torch.float32):
     (64, 0, 64, 2, 32, 32, True),      # 16x16 halo-tile kernel
     (64, 64, 128, 1, 16, 48, True),    # halo kernel, two sources, BN = 128
     (128, 0, 256, 2, 20, 24, True),    # halo kernel, partial edge tiles
+    (32, 0, 64, 2, 24, 20, True),      # one fp32 channel chunk: weights-resident persistent kernel
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_conv3x3_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
@@ -129,7 +130,7 @@ def test_conv3x3_fwd_small_c_nchw():
 
 @pytest.mark.parametrize("cin,cout,split,h,w", [(64, 64, 0, 8, 8), (128, 64, 64, 8, 8), (512, 256, 256, 8, 8),
                                                 (64, 128, 0, 8, 8), (64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
-                                                (256, 128, 128, 16, 48)])
+                                                (256, 128, 128, 16, 48), (64, 32, 0, 24, 20), (128, 32, 64, 16, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_conv3x3_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     halo_wgs(wgs)
@@ -462,6 +463,8 @@ def test_first_conv_fwd_and_wgrad(dt, cin, n, h, w):
 
 @pytest.mark.parametrize("cin0,cin1,cout,n,h,w", [
     (128, 0, 128, 2, 20, 72),    # partial tiles in both directions
+    (64, 0, 64, 2, 40, 36),      # one channel chunk: weights-resident persistent kernel
+    (64, 0, 128, 3, 24, 24),     # one chunk, two 64-column tiles
     (128, 128, 256, 1, 33, 40),  # two sources (torch.cat), two column tiles
     (256, 0, 512, 2, 32, 32),    # four chunks, four column tiles
 ])
@@ -499,7 +502,8 @@ def test_conv3x3_bf16_persist_fwd_stats(cin0, cin1, cout, n, h, w, wgs, halo_wgs
 
 
 @pytest.mark.parametrize("cin,cout,split,h,w", [(256, 128, 0, 20, 40), (256, 128, 128, 16, 64),
-                                                (512, 256, 256, 32, 32)])
+                                                (512, 256, 256, 32, 32), (64, 64, 0, 20, 40),
+                                                (128, 64, 64, 24, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_conv3x3_bf16_persist_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     """bf16 data gradient on the persistent halo kernel: plain with the producer's BN-backward sums,
