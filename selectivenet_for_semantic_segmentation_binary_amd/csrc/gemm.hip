@@ -442,23 +442,77 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
   const bool pin = pk < P.K, qin = qk < Q.K;
 
   uint4 rp[PI], rq[PJ];
-  auto load_stage = [&](int64_t m_base) {
+  // Vector path (!SMALL): the raw 16-B loads are issued unconditionally (out-of-image / padding rows
+  // clamped to pixel 0) and stay in flight across the current stage's MFMAs; the producer's
+  // BN+ReLU and the zeroing are applied when the stage is written to LDS. (Transforming right after
+  // the load made every stage wait out the full global latency.)
+  const SrcArg psa = pick_src(P, ps), qsa = pick_src(Q, qs);
+  float psc[8], psh[8], qsc[8], qsh[8];
+  unsigned pok = 0, qok = 0;  // bit i: staged row i is a real (non-padding) pixel
+  if constexpr (!SMALL) {
 #pragma unroll
-    for (int i = 0; i < PI; ++i) {
-      const int64_t m = m_base + pr + RPI * i;
-      rp[i] = gather_vec8_bf16(P, m < me ? m : P.M, pk, ptap, ps, pch, pvec, pin);
+    for (int e = 0; e < 8; ++e) {
+      psc[e] = psa.scale && pin ? psa.scale[pch + e] : 1.0f;
+      psh[e] = psa.scale && pin ? psa.shift[pch + e] : 0.0f;
+      qsc[e] = qsa.scale && qin ? qsa.scale[qch + e] : 1.0f;
+      qsh[e] = qsa.scale && qin ? qsa.shift[qch + e] : 0.0f;
     }
+  }
+  auto raw_row = [&](const GatherArg& g, const SrcArg& sa, int64_t m, int tap, int c, bool in, unsigned& ok,
+                     int bit) __attribute__((always_inline)) {
+    int64_t pix = (in && m < me) ? src_index(g, m, tap) : -1;
+    ok |= (pix >= 0 ? 1u : 0u) << bit;
+    pix = pix >= 0 ? pix : 0;
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(sa.data) + pix * sa.C + c);
+  };
+  auto finish = [&](uint4 raw, bool ok, const SrcArg& sa, const float* sc, const float* sh)
+      __attribute__((always_inline)) {
+    if (!ok) return make_uint4(0, 0, 0, 0);
+    if (!sa.scale) return raw;
+    __bf16 v[8];
+    __builtin_memcpy(v, &raw, 16);
 #pragma unroll
-    for (int i = 0; i < PJ; ++i) {
-      const int64_t m = m_base + qr + RPJ * i;
-      rq[i] = gather_vec8_bf16(Q, m < me ? m : Q.M, qk, qtap, qs, qch, qvec, qin);
+    for (int e = 0; e < 8; ++e) {
+      float f = (float)v[e] * sc[e] + sh[e];
+      if (sa.relu) f = fmaxf(f, 0.0f);
+      v[e] = (__bf16)f;
+    }
+    __builtin_memcpy(&raw, v, 16);
+    return raw;
+  };
+  auto load_stage = [&](int64_t m_base) {
+    if constexpr (!SMALL) {
+      pok = qok = 0;
+#pragma unroll
+      for (int i = 0; i < PI; ++i) rp[i] = raw_row(P, psa, m_base + pr + RPI * i, ptap, pch, pin, pok, i);
+#pragma unroll
+      for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+    } else {
+#pragma unroll
+      for (int i = 0; i < PI; ++i) {
+        const int64_t m = m_base + pr + RPI * i;
+        rp[i] = gather_vec8_bf16(P, m < me ? m : P.M, pk, ptap, ps, pch, pvec, pin);
+      }
+#pragma unroll
+      for (int i = 0; i < PJ; ++i) {
+        const int64_t m = m_base + qr + RPJ * i;
+        rq[i] = gather_vec8_bf16(Q, m < me ? m : Q.M, qk, qtap, qs, qch, qvec, qin);
+      }
     }
   };
   auto store_stage = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < PI; ++i) *reinterpret_cast<uint4*>(&Ps[buf][pr + RPI * i][pc * 8]) = rp[i];
+    for (int i = 0; i < PI; ++i) {
+      uint4 v = rp[i];
+      if constexpr (!SMALL) v = finish(v, (pok >> i) & 1u, psa, psc, psh);
+      *reinterpret_cast<uint4*>(&Ps[buf][pr + RPI * i][pc * 8]) = v;
+    }
 #pragma unroll
-    for (int i = 0; i < PJ; ++i) *reinterpret_cast<uint4*>(&Qs[buf][qr + RPJ * i][qc * 8]) = rq[i];
+    for (int i = 0; i < PJ; ++i) {
+      uint4 v = rq[i];
+      if constexpr (!SMALL) v = finish(v, (qok >> i) & 1u, qsa, qsc, qsh);
+      *reinterpret_cast<uint4*>(&Qs[buf][qr + RPJ * i][qc * 8]) = v;
+    }
   };
 
   f32x16 acc[MT][NT];
