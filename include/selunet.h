@@ -141,6 +141,15 @@ const char* selunet_gemm_kernel_name(const selunet_gather* a, const selunet_gath
  * Replaces the weight-gradient of conv2d / conv_transpose2d (train.py:208 backward). */
 int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out,
                        int32_t dtype, void* stream);
+/* Deterministic variant: the pixel splits write their partial sums to the workspace `ws`
+ * (selunet_gemm_wgrad_ws_bytes bytes; fp32 [splits][ni][ld]) and a reduction kernel sums them in
+ * a fixed order into out, which is overwritten (no zeroing needed; pad columns become 0). Operands
+ * without a split-partials path (fp32) report 0 bytes; out is then zeroed and accumulated with
+ * atomics inside the call. Removes the fp32 atomic traffic (~150 MB per 3x3 layer) of
+ * selunet_gemm_wgrad. */
+int64_t selunet_gemm_wgrad_ws_bytes(const selunet_gather* p, const selunet_gather* q, int32_t dtype);
+int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gather* q, float* out, float* ws,
+                          int64_t ws_bytes, int32_t dtype, void* stream);
 /* Row stride of the packed wgrad output for a Q operand with kq columns (kq rounded up to
  * the column tile); `out` must be [ni][selunet_wgrad_ld(kq)], the pad columns are garbage-free
  * zeros when out was zeroed. */

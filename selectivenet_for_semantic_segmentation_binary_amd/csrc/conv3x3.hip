@@ -603,7 +603,8 @@ constexpr int WPIXT = WTH * WTW;                 // 128 pixels
 template <int BI>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int co_tiles, int ci_chunks,
-                          int64_t tiles_per_split, int tiles_x, int tiles_y, int64_t total_tiles) {
+                          int64_t tiles_per_split, int tiles_x, int tiles_y, int64_t total_tiles,
+                          float* __restrict__ ws, int64_t ws_stride) {
   constexpr int LDP = BI + 32;                   // dY tile row stride (elements)
   constexpr int LDX = 64 + 32;                   // halo row stride (elements)
   constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
@@ -789,7 +790,8 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        atomicAdd(out + (int64_t)i * ldo + j, acc[t][r]);
+        if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[t][r];  // this split's partial
+        else atomicAdd(out + (int64_t)i * ldo + j, acc[t][r]);
       }
     }
   }
@@ -804,22 +806,36 @@ bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dty
   return true;
 }
 
-int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, hipStream_t st) {
+// pixel-tile splits of the halo weight gradient: ~512 workgroups over (co tile, ci chunk, split)
+int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
+  const int ni = p.K;
+  const int bi = ni % 128 == 0 ? 128 : 64;
+  const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
+  const int64_t total = (int64_t)q.n * cdiv(q.w, WTW) * cdiv(q.h, WTH);
+  const int64_t want = std::max<int64_t>(1, cdiv(512, (int64_t)co_tiles * ci_chunks));
+  const int64_t per = cdiv(total, std::min(total, want));
+  if (per_out) *per_out = per;
+  return cdiv(total, per);
+}
+
+// ws == nullptr: fp32 atomics into out (zeroed by the caller). Otherwise every split writes its
+// partial to ws[split][ni][ldo] (ws_stride = ni * ldo floats) and the caller reduces the splits.
+int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, hipStream_t st) {
   const int ni = p.K;
   const int bi = ni % 128 == 0 ? 128 : 64;
   const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
   const int tiles_x = (int)cdiv(q.w, WTW), tiles_y = (int)cdiv(q.h, WTH);
   const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
-  const int64_t want = std::max<int64_t>(1, cdiv(512, (int64_t)co_tiles * ci_chunks));
-  const int64_t per = cdiv(total, std::min(total, want));
-  const int64_t splits = cdiv(total, per);
+  int64_t per;
+  const int64_t splits = conv3x3_wgrad_halo_splits(p, q, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
+  const int64_t stride = (int64_t)ni * ldo;
   if (bi == 128)
     hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
-                       ci_chunks, per, tiles_x, tiles_y, total);
+                       ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
   else
     hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<64>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
-                       ci_chunks, per, tiles_x, tiles_y, total);
+                       ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
   return check_launch("conv3x3_wgrad_halo");
 }
 

@@ -396,7 +396,7 @@ __device__ __forceinline__ uint4 gather_vec8_bf16(const GatherArg& g, int64_t m,
 template <int BI, int BJ, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
 gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk, int tiles_j,
-                       int tiles) {
+                       int tiles, float* __restrict__ ws, int64_t ws_stride) {
   constexpr int KM = 64;                           // pixels per stage
   constexpr int PADE = 32;                         // 64 B row pad (bank spread for tr reads)
   constexpr int LDI = BI + PADE, LDJ = BJ + PADE;  // row strides in elements
@@ -567,7 +567,8 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + wi * WI + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
+        if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[a][b][r];
+        else atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
       }
     }
 }
@@ -622,7 +623,15 @@ template <typename T, int BN, bool SMALL>
 static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st);
 template <typename T, int BI, int BJ, bool SMALL>
 static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
-                              hipStream_t st);
+                              float* ws, hipStream_t st);
+
+// pixel splits of the generic weight gradient (rows per split a multiple of the 64-pixel stage)
+static int64_t wgrad_splits(int64_t M, int tiles, int64_t* mchunk_out) {
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(2048, tiles)));
+  const int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
+  if (mchunk_out) *mchunk_out = mchunk;
+  return cdiv(M, mchunk);
+}
 
 template <typename T, int BN>
 static void launch_gather(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
@@ -643,26 +652,24 @@ static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_p
 
 template <typename T, int BI, int BJ>
 static void launch_wgrad(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
-                         hipStream_t st) {
-  if (p.small || q.small) launch_wgrad_impl<T, BI, BJ, true>(p, q, out, ldo, ni, nj_pad, st);
-  else launch_wgrad_impl<T, BI, BJ, false>(p, q, out, ldo, ni, nj_pad, st);
+                         hipStream_t st, float* ws = nullptr) {
+  if (p.small || q.small) launch_wgrad_impl<T, BI, BJ, true>(p, q, out, ldo, ni, nj_pad, ws, st);
+  else launch_wgrad_impl<T, BI, BJ, false>(p, q, out, ldo, ni, nj_pad, ws, st);
 }
 
 template <typename T, int BI, int BJ, bool SMALL>
 static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out, int ldo, int ni, int nj_pad,
-                              hipStream_t st) {
+                              float* ws, hipStream_t st) {
   const int tiles_j = nj_pad / BJ;
   const int tiles = (ni / BI) * tiles_j;
-  const int64_t M = p.M;
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(2048, tiles)));
-  int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
-  splits = cdiv(M, mchunk);
+  int64_t mchunk;
+  const int64_t splits = wgrad_splits(p.M, tiles, &mchunk);
   if constexpr (std::is_same<T, float>::value)
     hipLaunchKernelGGL((gemm_wgrad_kernel<T, BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q, out,
                        ldo, mchunk, tiles_j, tiles);
   else
     hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q,
-                       out, ldo, mchunk, tiles_j, tiles);
+                       out, ldo, mchunk, tiles_j, tiles, ws, (int64_t)ni * ldo);
 }
 
 }  // namespace selunet
@@ -757,23 +764,66 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
   return check_launch("gemm_gather");
 }
 
-extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out, int32_t dtype,
-                                  void* stream) {
-  SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
+// Deterministic split reduction of the weight-gradient partials: out[i][j] = sum_s ws[s][i][j]
+// for j < kq (fixed split order), 0 in the pad columns.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int64_t splits, int64_t stride, int ni, int ldo,
+                                    int kq, float* __restrict__ out) {
+  const int64_t n4 = (int64_t)ni * ldo / 4;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n4; v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = v * 4;
+    const int j = (int)(e % ldo);
+    f32x4 acc = {0, 0, 0, 0};
+    if (j < kq) {
+      for (int64_t sp = 0; sp < splits; ++sp) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(ws + sp * stride + e);
+        acc += x;
+      }
+      if (j + 4 > kq)
+        for (int u = 0; u < 4; ++u)
+          if (j + u >= kq) acc[u] = 0.0f;
+    }
+    *reinterpret_cast<f32x4*>(out + e) = acc;
+  }
+}
+
+struct WgradPlan {
   GatherArg gp, gq;
+  int ni, bj, nj_pad;
+  bool halo;
+  int64_t splits;  // 0: no split-partials path (fp32 / atomics only)
+};
+
+static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t dtype, WgradPlan& w) {
+  SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
   const int vec = dtype == SELUNET_F32 ? 4 : 8;  // elements per staged vector
-  if (int rc = make_gather(p, dtype, gp, vec)) return rc;
-  if (int rc = make_gather(q, dtype, gq, vec)) return rc;
-  SELUNET_REQUIRE(out != nullptr, "out is NULL");
-  SELUNET_REQUIRE(gp.M == gq.M && p->n == q->n && p->h == q->h && p->w == q->w, "P and Q must share the row grid");
-  SELUNET_REQUIRE(gp.K % 64 == 0, "P columns (%d) must be a multiple of 64", gp.K);
-  SELUNET_REQUIRE(gp.small == 0, "P must be vector-gatherable");
-  const int ni = gp.K;
-  const int bj = (gq.K % 128 == 0 || gq.K > 512) ? 128 : 64;
-  const int nj_pad = (int)(cdiv(gq.K, bj) * bj);
-  hipStream_t st = as_stream(stream);
-  if (halo_enabled() && conv3x3_wgrad_halo_eligible(gp, gq, dtype))
-    return conv3x3_wgrad_halo_launch(gp, gq, out, nj_pad, st);
+  if (int rc = make_gather(p, dtype, w.gp, vec)) return rc;
+  if (int rc = make_gather(q, dtype, w.gq, vec)) return rc;
+  SELUNET_REQUIRE(w.gp.M == w.gq.M && p->n == q->n && p->h == q->h && p->w == q->w, "P and Q must share the row grid");
+  SELUNET_REQUIRE(w.gp.K % 64 == 0, "P columns (%d) must be a multiple of 64", w.gp.K);
+  SELUNET_REQUIRE(w.gp.small == 0, "P must be vector-gatherable");
+  w.ni = w.gp.K;
+  w.bj = (w.gq.K % 128 == 0 || w.gq.K > 512) ? 128 : 64;
+  w.nj_pad = (int)(cdiv(w.gq.K, w.bj) * w.bj);
+  w.halo = halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, dtype);
+  w.splits = 0;
+  if (dtype == SELUNET_BF16) {
+    if (w.halo) {
+      w.splits = conv3x3_wgrad_halo_splits(w.gp, w.gq, nullptr);
+    } else {
+      const int bi = w.ni % 128 == 0 ? 128 : 64;
+      w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
+    }
+  }
+  return 0;
+}
+
+static void launch_wgrad_any(const WgradPlan& w, float* out, float* ws, int32_t dtype, hipStream_t st) {
+  const GatherArg &gp = w.gp, &gq = w.gq;
+  const int ni = w.ni, nj_pad = w.nj_pad, bj = w.bj;
+  if (w.halo) {
+    conv3x3_wgrad_halo_launch(gp, gq, out, nj_pad, ws, st);
+    return;
+  }
   const bool bi128 = ni % 128 == 0;
   // out is [ni][nj_pad] where nj_pad = roundup(Kq, 64 or 128): see selunet_wgrad_ld()
   if (dtype == SELUNET_F32) {
@@ -782,12 +832,48 @@ extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather*
     else if (bi128) launch_wgrad<float, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
     else launch_wgrad<float, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
   } else {
-    if (bi128 && bj == 128) launch_wgrad<__bf16, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else if (bj == 128) launch_wgrad<__bf16, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else if (bi128) launch_wgrad<__bf16, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else launch_wgrad<__bf16, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    if (bi128 && bj == 128) launch_wgrad<__bf16, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else if (bj == 128) launch_wgrad<__bf16, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else if (bi128) launch_wgrad<__bf16, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else launch_wgrad<__bf16, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
   }
+}
+
+extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* out, int32_t dtype,
+                                  void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad(p, q, dtype, w)) return rc;
+  SELUNET_REQUIRE(out != nullptr, "out is NULL");
+  launch_wgrad_any(w, out, nullptr, dtype, as_stream(stream));
   return check_launch("gemm_wgrad");
+}
+
+extern "C" int64_t selunet_gemm_wgrad_ws_bytes(const selunet_gather* p, const selunet_gather* q, int32_t dtype) {
+  WgradPlan w;
+  if (plan_wgrad(p, q, dtype, w)) return -1;
+  return w.splits * (int64_t)w.ni * w.nj_pad * 4;
+}
+
+extern "C" int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gather* q, float* out, float* ws,
+                                     int64_t ws_bytes, int32_t dtype, void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad(p, q, dtype, w)) return rc;
+  SELUNET_REQUIRE(out != nullptr, "out is NULL");
+  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  hipStream_t st = as_stream(stream);
+  if (need == 0) {  // no split-partials path for these operands: zero + atomics
+    SELUNET_REQUIRE(hipMemsetAsync(out, 0, (size_t)w.ni * w.nj_pad * 4, st) == hipSuccess, "hipMemsetAsync failed");
+    launch_wgrad_any(w, out, nullptr, dtype, st);
+    return check_launch("gemm_wgrad_ws");
+  }
+  SELUNET_REQUIRE(ws != nullptr && ws_bytes >= need, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                  (long long)ws_bytes);
+  launch_wgrad_any(w, out, ws, dtype, st);
+  const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 256), 4096));
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, w.splits, (int64_t)w.ni * w.nj_pad,
+                     w.ni, w.nj_pad, w.gq.K, out);
+  return check_launch("gemm_wgrad_ws");
 }
 
 // leading dimension of the packed wgrad output for a Q operand with kq columns

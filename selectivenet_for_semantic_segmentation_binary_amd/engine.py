@@ -107,6 +107,7 @@ class Engine:
         self.code = K.dtype_code(dt)
         self.bke = 128 // torch.empty((), dtype=dt).element_size()
         self.plans_enabled = os.environ.get("SELUNET_NO_PLANS", "0") != "1"
+        self.deterministic = os.environ.get("SELUNET_DETERMINISTIC", "0") == "1"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -117,6 +118,21 @@ class Engine:
     @property
     def stream(self):
         return K.stream_ptr()
+
+    def _wgrad(self, gp, gq, packed):
+        """packed = P^T Q (weight gradient, fp32 [ni][ld]), overwritten: zero + fp32 atomics over the
+        pixel splits (default), or with SELUNET_DETERMINISTIC=1 (bf16) split partials in a workspace
+        reduced in a fixed order — bit-reproducible, measured 1-3% slower per step (the atomics
+        overlap other workgroups' MFMAs; the extra reduction pass does not)."""
+        if not self.deterministic:
+            K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
+            K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
+            return
+        wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, self.code)
+        if wsb < 0:
+            raise RuntimeError(f"selunet_gemm_wgrad_ws_bytes: {K.load().selunet_last_error().decode()}")
+        ws = K.keep(torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=packed.device)) if wsb > 0 else None
+        K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, self.code, self.stream)
 
     def pack_weights(self, P, need_dgrad=True):
         """fp32 master weights -> GEMM operand layouts in the compute dtype."""
@@ -326,10 +342,9 @@ class Engine:
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
         packed = K.keep(torch.empty(co, ld, dtype=torch.float32, device=dev))
-        K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
-        K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
+        self._wgrad(gp, gq, packed)
         K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
         if not need_dgrad:
             return None
@@ -363,10 +378,9 @@ class Engine:
         self._reduce(du.slab, du.rows, co, out32=G[f"{name}.bias"])
         ld = K.query("selunet_wgrad_ld", 4 * co)
         packed = K.keep(torch.empty(ci, ld, dtype=torch.float32, device=dev))
-        K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
         gp = K.gather(n, h, w, 1, prev.src())
         gq = K.gather(n, h, w, 4, K.source(du.t, co))
-        K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
+        self._wgrad(gp, gq, packed)
         K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
         dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))

@@ -359,6 +359,23 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
+def wgrad_ws(gp, gq, packed_atomic, dtype=K.BF16):
+    """The deterministic split-reduced weight gradient (selunet_gemm_wgrad_ws) into a poisoned
+    buffer: equal to the atomic result up to fp32 summation order, and bit-identical on a rerun."""
+    outs = []
+    for _ in range(2):
+        wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, dtype)
+        assert wsb >= 0
+        ws = torch.empty(max(wsb // 4, 1), device=DEV)
+        out = torch.full_like(packed_atomic, float("nan"))
+        K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(out), K.ptr(ws), wsb, dtype, K.stream_ptr())
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert rel(outs[0].cpu(), packed_atomic.cpu()) < 1e-5
+    return outs[0]
+
+
 @pytest.mark.parametrize("cin0,cin1,cout,small,h,w", [(64, 0, 64, False, 16, 16), (64, 64, 128, False, 16, 16),
                                                       (256, 0, 512, False, 16, 16), (3, 0, 64, True, 16, 16),
                                                       (128, 0, 64, False, 20, 40), (64, 128, 64, False, 24, 17)])
@@ -399,8 +416,9 @@ def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small, h, w, wgs, halo_wgs):
     dyd = d(nhwc(dy)).bfloat16()
     ld = K.query("selunet_wgrad_ld", 9 * cin)
     packed = torch.zeros(cout, ld, device=DEV)
-    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs),
-           K.ptr(packed), K.BF16, K.stream_ptr())
+    gp, gq = K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs)
+    K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), K.BF16, K.stream_ptr())
+    wgrad_ws(gp, gq, packed)
     gwd = torch.empty(cout, cin, 3, 3, device=DEV)
     K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cout, cin, ld, K.ptr(gwd), K.stream_ptr())
     assert rel(gwd.cpu(), gw) < 1e-3  # inputs exactly bf16, fp32 accumulation
@@ -417,8 +435,9 @@ def test_convT_bf16_wgrad():
     dud = nhwc(dy).to(DEV).bfloat16()
     ld = K.query("selunet_wgrad_ld", 4 * cout)
     packed = torch.zeros(cin, ld, device=DEV)
-    K.call("selunet_gemm_wgrad", K.gather(n, h, w, 1, K.source(xd, cin)), K.gather(n, h, w, 4, K.source(dud, cout)),
-           K.ptr(packed), K.BF16, K.stream_ptr())
+    gp, gq = K.gather(n, h, w, 1, K.source(xd, cin)), K.gather(n, h, w, 4, K.source(dud, cout))
+    K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), K.BF16, K.stream_ptr())
+    wgrad_ws(gp, gq, packed)
     gwd = torch.empty(cin, cout, 2, 2, device=DEV)
     K.call("selunet_unpack_convT_grad", K.ptr(packed), cin, cout, K.ptr(gwd), K.stream_ptr())
     assert rel(gwd.cpu(), gw) < 1e-3
