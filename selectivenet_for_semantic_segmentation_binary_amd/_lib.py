@@ -204,10 +204,17 @@ class Plan:
                 pos.append(i)
         self.calls.append((name, fn, tuple(args), tuple(pos)))
 
-    def replay(self, slots):
+    def record_marker(self, tag):
+        self.calls.append((None, None, tag, ()))
+
+    def replay(self, slots, on_marker=None):
         base = {n: t.data_ptr() for n, t in slots.items() if t is not None}
         L = load()
         for name, fn, args, pos in self.calls:
+            if name is None:  # marker: host-side hook between launches (e.g. a gradient bucket's all-reduce)
+                if on_marker is not None:
+                    on_marker(args)
+                continue
             if pos:
                 a = list(args)
                 for i in pos:
@@ -232,6 +239,36 @@ def _check_struct(st, slot_of, name):
 
 
 _REC = None
+
+
+_MARKER_CB = None
+
+
+def marker(tag):
+    """A point in the launch sequence where host code may act (the gradients of a layer are
+    enqueued): calls the active marker callback now and, while recording, stores the marker in the
+    plan so replays call their callback at the same point."""
+    if _REC is not None:
+        _REC.record_marker(tag)
+    if _MARKER_CB is not None:
+        _MARKER_CB(tag)
+
+
+class marker_callback:
+    """Context manager installing the callback `marker` calls during a (recorded) pass."""
+
+    def __init__(self, cb):
+        self.cb = cb
+
+    def __enter__(self):
+        global _MARKER_CB
+        self.prev, _MARKER_CB = _MARKER_CB, self.cb
+        return self
+
+    def __exit__(self, *exc):
+        global _MARKER_CB
+        _MARKER_CB = self.prev
+        return False
 
 
 def keep(t):

@@ -338,6 +338,7 @@ class Engine:
             self._reduce(slab, rows, co * FIRST_KPAD, out32=packed)
             K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, cin, FIRST_KPAD, K.ptr(G[f"{name}.0.weight"]),
                    self.stream)
+            K.marker(("grads", name))
             return None
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
@@ -346,6 +347,7 @@ class Engine:
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
         self._wgrad(gp, gq, packed)
         K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
+        K.marker(("grads", name))
         if not need_dgrad:
             return None
         _, wd, _ = ctx.wpack[name]
@@ -382,6 +384,7 @@ class Engine:
         gq = K.gather(n, h, w, 4, K.source(du.t, co))
         self._wgrad(gp, gq, packed)
         K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
+        K.marker(("grads", name))
         dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))
         rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
@@ -400,23 +403,28 @@ class Engine:
                K.ptr(dp.t), K.ptr(dskip), K.ptr(dz), bnb, self.code, self.stream)
         return DGrad(dz, slab, rows)
 
-    def backward(self, ctx, P, G, g_heads, flat):
+    def backward(self, ctx, P, G, g_heads, flat, on_grads=None):
         """g_heads: list of fp32 [N,H,W] grads of (out[, select, aux]) (None -> zeros). G: the
-        parameter-gradient views (reference layouts) of the flat fp32 buffer `flat`, written here."""
+        parameter-gradient views (reference layouts) of the flat fp32 buffer `flat`, written here.
+        on_grads(layer_name) is called on the host as soon as a layer's parameter gradients are
+        enqueued (heads first, encoder_layer_1_1 last), e.g. to start their all-reduce while the
+        rest of the backward runs."""
         g_heads = [g.contiguous() if g is not None else None for g in g_heads]
         e = ctx.entry
+        cb = (lambda tag: on_grads(tag[1])) if on_grads is not None else None
         if e is None:
-            self._backward_impl(ctx, P, G, g_heads)
+            with K.marker_callback(cb):
+                self._backward_impl(ctx, P, G, g_heads)
             return
         pattern = tuple(g is None for g in g_heads)
         slots = {"x": ctx.x, "flat": flat, **{f"g{i}": g for i, g in enumerate(g_heads) if g is not None}}
         plan = e.bwd.get(pattern)
         try:
             if plan is not None:
-                plan.replay(slots)
+                plan.replay(slots, on_marker=cb)
             else:
                 plan = K.Plan(slots)
-                with K.recording(plan):
+                with K.recording(plan), K.marker_callback(cb):
                     self._backward_impl(ctx, P, G, g_heads)
                 e.bwd[pattern] = plan
         finally:
@@ -448,6 +456,7 @@ class Engine:
             assert G[f"{h}.weight"].data_ptr() == hw0.data_ptr() + i * 65 * 4
             assert G[f"{h}.bias"].data_ptr() == hw0.data_ptr() + (i * 65 + 64) * 4
         self._reduce(slab, rows, nh * 65, out32=hw0)
+        K.marker(("grads", "heads"))
 
         e12, e22, e32 = bn["encoder_layer_1_2"], bn["encoder_layer_2_2"], bn["encoder_layer_3_2"]
         u1, u2, u3 = ctx.ups["unpool1"], ctx.ups["unpool2"], ctx.ups["unpool3"]

@@ -116,16 +116,20 @@ class _UNetBFunction(torch.autograd.Function):
         dev = g_heads[0].device if g_heads[0] is not None else next(iter(P.values())).device
         total = sum(P[n].numel() for n in names)
         flat = torch.empty(total, dtype=torch.float32, device=dev)
-        G, off = {}, 0
+        G, off, layout = {}, 0, []
         for n in names:
             k = P[n].numel()
             G[n] = flat[off:off + k].view(P[n].shape)
+            layout.append((n, off, k))
             off += k
-        ctx.eng.backward(ctx.ectx, P, G, list(g_heads), flat)
+        # DataParallel reduce-add of the replica gradients: bucketed all-reduces issued while the
+        # backward of the shallower layers still runs
+        bucketer = parallel.GradBucketer(flat, layout) if parallel.is_initialized() else None
+        ctx.eng.backward(ctx.ectx, P, G, list(g_heads), flat, on_grads=bucketer.ready if bucketer else None)
         ctx.release.detach()
         ctx.ectx = None
-        if parallel.is_initialized():
-            parallel.allreduce_grads(flat)  # DataParallel reduce-add of replica gradients
+        if bucketer is not None:
+            bucketer.finish()
         return (None, None, *[G[n] for n in names])
 
 

@@ -87,6 +87,66 @@ def allreduce_grads(flat: torch.Tensor, bucket_elems: int = 1 << 22) -> torch.Te
     return flat
 
 
+def grad_layer(param_name: str) -> str:
+    """The engine layer whose backward writes this parameter's gradient (Engine.backward on_grads
+    tags): the module prefix, or "heads" for the 1x1 heads (reduced together)."""
+    mod = param_name.split(".")[0]
+    return "heads" if mod in ("conv1x1", "conv_select", "conv_aux") else mod
+
+
+class GradBucketer:
+    """SUM all-reduce of the flat gradient buffer in buckets overlapped with the backward.
+
+    Buckets are runs of consecutive parameters (flat = registration order) of at least
+    `bucket_elems` floats, cut at parameter boundaries and formed from the END of the buffer: the
+    backward produces the head and decoder gradients first and encoder_layer_1_1's last. A bucket's
+    all-reduce is enqueued (async, RCCL's stream waits on the compute stream up to that point) as
+    soon as every layer it covers has reported its gradients through `ready`; `finish` enqueues
+    anything left and makes the current stream wait for all of them. Every rank reports the layers
+    in the same order, so the collectives are issued in the same order everywhere."""
+
+    def __init__(self, flat: torch.Tensor, layout, bucket_elems: int = 1 << 20):
+        # layout: [(param_name, offset, numel)] in flat order
+        self.flat = flat
+        self.buckets = []          # [lo, hi, pending layer set]
+        self.works = []
+        cur_hi, cur_lo, layers = None, None, set()
+        for name, off, n in reversed(list(layout)):
+            if cur_hi is None:
+                cur_hi = off + n
+            cur_lo = off
+            layers.add(grad_layer(name))
+            if cur_hi - cur_lo >= bucket_elems:
+                self.buckets.append([cur_lo, cur_hi, layers])
+                cur_hi, layers = None, set()
+        if cur_hi is not None:
+            self.buckets.append([cur_lo, cur_hi, layers])
+        self.launched = [False] * len(self.buckets)
+
+    def _launch(self, i):
+        lo, hi, _ = self.buckets[i]
+        self.launched[i] = True
+        if is_initialized():
+            self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_STATE["group"],
+                                              async_op=True))
+
+    def ready(self, layer: str):
+        for i, b in enumerate(self.buckets):
+            if not self.launched[i] and layer in b[2]:
+                b[2].discard(layer)
+                if not b[2]:
+                    self._launch(i)
+
+    def finish(self) -> torch.Tensor:
+        for i in range(len(self.buckets)):
+            if not self.launched[i]:
+                self._launch(i)
+        for w in self.works:
+            w.wait()
+        self.works = []
+        return self.flat
+
+
 def broadcast_buffers(module: torch.nn.Module):
     if not is_initialized():
         return

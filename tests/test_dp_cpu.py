@@ -162,3 +162,48 @@ def test_sharded_selective_loss_equals_dataparallel(tmp_path):
     # replica-0 BN buffers are the ones DataParallel keeps
     for k, v in r0["buffers"].items():
         np.testing.assert_allclose(v.numpy(), buffers[k].detach().numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+# ----------------------------------------------------------------------------- overlapped buckets
+def _bucketer_worker(rank, world, port, out):
+    _init(rank, world, port)
+    import selectivenet_for_semantic_segmentation_binary_amd.layout as L
+    specs = L.param_specs("RGB", True)
+    names = [k for k, _, _, _ in specs]
+    shapes = {k: shp for k, shp, _, _ in specs}
+    layout, off = [], 0
+    for n in names:
+        k = int(np.prod(shapes[n]))
+        layout.append((n, off, k))
+        off += k
+    g = torch.Generator().manual_seed(100 + rank)
+    flat = torch.randn(off, generator=g)
+    want = flat.clone()
+    dist.all_reduce(want)
+    b = parallel.GradBucketer(flat, layout, bucket_elems=1 << 18)
+    assert len(b.buckets) > 4
+    # the engine's backward order: heads, decoder 1_1 ... 4_2, encoder 3_2 ... 1_1
+    order = ["heads", "decoder_layer_1_1", "decoder_layer_1_2", "unpool1", "decoder_layer_2_1",
+             "decoder_layer_2_2", "unpool2", "decoder_layer_3_1", "decoder_layer_3_2", "unpool3",
+             "decoder_layer_4_1", "decoder_layer_4_2", "encoder_layer_3_2", "encoder_layer_3_1",
+             "encoder_layer_2_2", "encoder_layer_2_1", "encoder_layer_1_2", "encoder_layer_1_1"]
+    assert set(order) == {parallel.grad_layer(n) for n in names}
+    launched_before_last = None
+    for i, layer in enumerate(order):
+        b.ready(layer)
+        if i == len(order) - 2:
+            launched_before_last = sum(b.launched)
+    b.finish()
+    out[rank] = (float((flat - want).abs().max()), launched_before_last, len(b.buckets))
+
+
+def test_grad_bucketer_overlapped_allreduce():
+    """Buckets close in backward order (all but the encoder_layer_1_1 one are issued before the last
+    layer reports) and the bucketed sum equals one all-reduce of the whole buffer."""
+    world = 2
+    out = mp.Manager().dict()
+    _spawn(_bucketer_worker, world, out)
+    for r in range(world):
+        err, before_last, nb = out[r]
+        assert err < 1e-5
+        assert before_last == nb - 1
