@@ -766,18 +766,27 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
 
 // Deterministic split reduction of the weight-gradient partials: out[i][j] = sum_s ws[s][i][j]
 // for j < kq (fixed split order), 0 in the pad columns.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int64_t splits, int64_t stride, int ni, int ldo,
-                                    int kq, float* __restrict__ out) {
+__global__ void __launch_bounds__(64) wgrad_reduce_kernel(const float* __restrict__ ws, int64_t splits,
+                                                          int64_t stride, int ni, int ldo, int kq,
+                                                          float* __restrict__ out) {
+  // one wave per block, 4 floats per lane, 16 split loads in flight per lane (the splits of one
+  // element are 4*stride bytes apart: latency, not bandwidth, bounds a one-load-at-a-time loop)
+  constexpr int U = 16;
   const int64_t n4 = (int64_t)ni * ldo / 4;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n4; v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = v * 4;
     const int j = (int)(e % ldo);
     f32x4 acc = {0, 0, 0, 0};
     if (j < kq) {
-      for (int64_t sp = 0; sp < splits; ++sp) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(ws + sp * stride + e);
-        acc += x;
+      int64_t sp = 0;
+      for (; sp + U <= splits; sp += U) {
+        f32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = *reinterpret_cast<const f32x4*>(ws + (sp + u) * stride + e);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += x[u];
       }
+      for (; sp < splits; ++sp) acc += *reinterpret_cast<const f32x4*>(ws + sp * stride + e);
       if (j + 4 > kq)
         for (int u = 0; u < 4; ++u)
           if (j + u >= kq) acc[u] = 0.0f;
@@ -870,8 +879,8 @@ extern "C" int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gath
                   (long long)ws_bytes);
   launch_wgrad_any(w, out, ws, dtype, st);
   const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 256), 4096));
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, w.splits, (int64_t)w.ni * w.nj_pad,
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64), 0, st, ws, w.splits, (int64_t)w.ni * w.nj_pad,
                      w.ni, w.nj_pad, w.gq.K, out);
   return check_launch("gemm_wgrad_ws");
 }

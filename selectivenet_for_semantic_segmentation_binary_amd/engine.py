@@ -107,7 +107,7 @@ class Engine:
         self.code = K.dtype_code(dt)
         self.bke = 128 // torch.empty((), dtype=dt).element_size()
         self.plans_enabled = os.environ.get("SELUNET_NO_PLANS", "0") != "1"
-        self.deterministic = os.environ.get("SELUNET_DETERMINISTIC", "0") == "1"
+        self.deterministic = os.environ.get("SELUNET_DETERMINISTIC", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -120,10 +120,11 @@ class Engine:
         return K.stream_ptr()
 
     def _wgrad(self, gp, gq, packed):
-        """packed = P^T Q (weight gradient, fp32 [ni][ld]), overwritten: zero + fp32 atomics over the
-        pixel splits (default), or with SELUNET_DETERMINISTIC=1 (bf16) split partials in a workspace
-        reduced in a fixed order — bit-reproducible, measured 1-3% slower per step (the atomics
-        overlap other workgroups' MFMAs; the extra reduction pass does not)."""
+        """packed = P^T Q (weight gradient, fp32 [ni][ld]), overwritten. bf16 (default): the pixel
+        splits write partials to a workspace reduced in a fixed order — bit-reproducible, and at
+        small per-GPU batches faster than the fp32 atomics it replaces (~150 MB of atomic adds per
+        3x3 layer, independent of the batch): +8% images/s at 16 images per GPU, equal at 128.
+        SELUNET_DETERMINISTIC=0 selects zero + atomics."""
         if not self.deterministic:
             K.call("selunet_memset", K.ptr(packed), 0, packed.numel() * 4, self.stream)
             K.call("selunet_gemm_wgrad", gp, gq, K.ptr(packed), self.code, self.stream)
