@@ -62,7 +62,7 @@ class KernelTimer:
     dispatches to (selunet_gemm_kernel_name), with its algorithmic FLOPs (2*M*N*K of the true,
     unpadded GEMM) and algorithmic HBM bytes (each operand tensor read once, output written once)."""
 
-    ENTRY = ("selunet_gemm_gather", "selunet_gemm_wgrad")
+    ENTRY = ("selunet_gemm_gather", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws")
 
     def __init__(self, esz):
         self.active = False
@@ -91,7 +91,10 @@ class KernelTimer:
             shape = f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
         else:
             gp, gq = args[0], args[1]
-            kname = K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, args[3]).decode()
+            dt = args[3] if name == "selunet_gemm_wgrad" else args[5]
+            kname = K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, dt).decode()
+            if name == "selunet_gemm_wgrad_ws" and args[4] > 0:
+                kname += "+reduce"  # (the entry point's time includes the split reduction)
             flops = 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             shape = f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
