@@ -207,3 +207,61 @@ def test_adam_matches_reference_algorithm():
     sd = opt.state_dict()
     ropt2 = torch.optim.Adam([r.detach().clone().requires_grad_() for r in ref], lr=1e-2)
     ropt2.load_state_dict(sd)  # checkpoint interchangeability (utils/net_utils.py:5-9)
+
+
+@pytest.mark.parametrize("input_type,n,h,w,selective", [
+    ("GH", 2, 32, 32, True),     # model.py:24-27: 'GH' inputs have 2 channels
+    ("RGB", 1, 32, 48, True),    # batch of one, non-square patches
+    ("RGB", 3, 48, 32, False),   # non-selective UNet_B, odd batch, non-square
+])
+def test_step_against_oracle_shapes(input_type, n, h, w, selective):
+    """One fp32 training step (forward, losses, backward) against the CPU oracle at shapes the
+    fixtures do not cover. Loss within 1e-4 relative of the oracle's fp32 run; gradients judged
+    as in check_step: relative-L2 error against the oracle's fp64 run no worse than
+    max(3 x the oracle fp32 run's own error, 1e-2) (ReLU / max-pool near-ties route
+    fp32 gradients differently under any change of summation order)."""
+    x, lab = make_batch(n, max(h, w), seed=11)
+    x = np.ascontiguousarray(x[:, :L.input_channels(input_type), :h, :w])
+    lab = np.ascontiguousarray(lab[:, :h, :w])
+    p = L.seeded_params(3, input_type, selective)
+    net = S.UNet_B(input_type, selective=selective)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    net = net.to(DEV).train()
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    outs = net(xt)
+    if selective:
+        out, sel, aux = outs
+        sl, _ = S.calc_selective_risk_image_b(out, sel, lt, lamb=2)
+        loss = S.BCEWithLogitsLoss()(aux, lt) + sl
+    else:
+        loss = S.BCEWithLogitsLoss()(outs, lt)
+    loss.backward()
+    torch.cuda.synchronize()
+
+    def oracle(dt):
+        params, buffers = O.make_state(3, input_type, selective)
+        params = {k: v.detach().to(dt).requires_grad_() for k, v in params.items()}
+        buffers = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in buffers.items()}
+        xo, lo = torch.tensor(x, dtype=dt), torch.tensor(lab, dtype=dt)
+        ro = O.forward(params, buffers, xo, selective, training=True)
+        if selective:
+            o2, s2, a2 = ro
+            sl2, _ = O.selective_risk_b_stable(o2, s2, lo, lamb=2)
+            l2 = O.bce_with_logits_mean(a2, lo) + sl2
+        else:
+            l2 = O.bce_with_logits_mean(ro, lo)
+        l2.backward()
+        return float(l2), {k: v.grad.double() for k, v in params.items()}
+
+    loss32, g32 = oracle(torch.float32)
+    _, g64 = oracle(torch.float64)
+    assert abs(loss.item() - loss32) < 1e-4 * max(1.0, abs(loss32))
+    for k, q in net.named_parameters():
+        if k in PRE_BN_BIAS:  # cancels inside training-mode BN: zero gradient on both sides
+            continue
+        nrm = float(g64[k].norm()) + 1e-30
+        err = float((q.grad.cpu().double() - g64[k]).norm()) / nrm
+        err_ref = float((g32[k] - g64[k]).norm()) / nrm
+        assert err <= max(3 * err_ref, 1e-2), (k, err, err_ref)
