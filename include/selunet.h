@@ -239,6 +239,29 @@ int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float*
                       const float* g2, void* dz, float* slab, const selunet_bn_bwd_stats* bnb,
                       int32_t dtype, void* stream);
 
+/* ---- N-output 1x1 heads (the CE `UNet`, model.py:106-191: conv1x1 64->n_cls, conv_select
+ * 64->2, conv_aux 64->n_cls) on relu(bn(y)), C = 64. Output k (k < n <= 8) is an fp32 plane
+ * set: pixel q of image i at plane[k][i * img_stride[k] + q] (q < hw), so the channels of
+ * NCHW [N, C, H, W] logits are planes base + c*hw with img_stride C*hw. */
+typedef struct selunet_head_planes {
+  int32_t n;               /* outputs (<= 8) */
+  int32_t hw;              /* pixels per image */
+  float* plane[8];         /* fwd: written; bwd: the incoming gradients (read) */
+  int64_t img_stride[8];
+  int32_t w_off[8];        /* bwd: slab column of output k's 64 weight grads */
+  int32_t b_off[8];        /*      and of its bias grad */
+  int32_t row_len;         /*      slab row length (the heads' segment of the gradient buffer) */
+} selunet_head_planes;
+/* w fp32 [n][64], b fp32 [n] */
+int selunet_heads_fwd_planes(const void* y, int64_t m, const float* scale, const float* shift,
+                             const float* w, const float* b, const selunet_head_planes* out,
+                             int32_t dtype, void* stream);
+/* dz[m][c] = sum_k g_k[m] w_k[c]; slab [selunet_channel_slab_rows(M)][row_len]: per output the
+ * sums g*z (64, at w_off) and g (at b_off); bnb as selunet_heads_bwd. */
+int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const float* shift,
+                             const float* w, const selunet_head_planes* grads, void* dz, float* slab,
+                             const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream);
+
 /* ---- losses ----------------------------------------------------------------------------- */
 /* calc_selective_risk_image_b (selective_loss.py:58-85), numerically stable form.
  * partials slab [selunet_loss_slab_rows(P)][2]: sum sigmoid(g), sum ell*sigmoid(g). */
@@ -259,6 +282,22 @@ int selunet_bce_partials(const float* logit, const float* target, int64_t p, flo
 int selunet_bce_finalize(const double* sums, double p_global, float* loss, void* stream);
 int selunet_bce_bwd(const float* logit, const float* target, int64_t p, double p_global,
                     const float* g_loss, float* d_logit, void* stream);
+/* Cross-entropy forms (CE `UNet`, n_cls = C <= 8): logits NCHW fp32 [N][C][hw], selection NCHW
+ * [N][2][hw], target int64 class indices [N][hw] (values outside [0, C) are clamped).
+ * calc_selective_risk_image (selective_loss.py:24-56): s = softmax(selection)[:, 1],
+ * ell = -log_softmax(output)[target]; partials slab [selunet_loss_slab_rows(N*hw)][2] = sum s,
+ * sum ell*s — finalized by selunet_selective_finalize exactly as the BCE form. */
+int selunet_ce_selective_partials(const float* out, const float* sel, const int64_t* target, int64_t n,
+                                  int32_t c, int64_t hw, float* slab, void* stream);
+int selunet_ce_selective_bwd(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                             int64_t hw, const float* state, float lamb, const float* g_loss,
+                             const float* g_coverage, float* d_out, float* d_sel, void* stream);
+/* torch.nn.CrossEntropyLoss() mean (train.py:80): slab [selunet_loss_slab_rows(N*hw)][1] = sum ell,
+ * finalized by selunet_bce_finalize (sum / P). */
+int selunet_ce_partials(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw,
+                        float* slab, void* stream);
+int selunet_ce_bwd(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw, double p_global,
+                   const float* g_loss, float* d_logit, void* stream);
 
 /* ---- torch.optim.Adam (train.py:90,209), multi-tensor ---------------------------------- */
 typedef struct selunet_adam_tensor {

@@ -43,6 +43,11 @@ class Epilogue(ctypes.Structure):
                 ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats)]
 
 
+class HeadPlanes(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("hw", c_int32), ("plane", c_void_p * 8), ("img_stride", c_int64 * 8),
+                ("w_off", c_int32 * 8), ("b_off", c_int32 * 8), ("row_len", c_int32)]
+
+
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
                 ("numel", c_int64), ("chunk_begin", c_int64)]
@@ -88,6 +93,13 @@ SIGNATURES = {
     "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),
     "selunet_heads_bwd": (c_int32, [P, c_int64, P, P, P, c_int32, P, P, P, P, P, ctypes.POINTER(BnBwdStats),
                                     c_int32, P]),
+    "selunet_heads_fwd_planes": (c_int32, [P, c_int64, P, P, P, P, ctypes.POINTER(HeadPlanes), c_int32, P]),
+    "selunet_heads_bwd_planes": (c_int32, [P, c_int64, P, P, P, ctypes.POINTER(HeadPlanes), P, P,
+                                           ctypes.POINTER(BnBwdStats), c_int32, P]),
+    "selunet_ce_selective_partials": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, P]),
+    "selunet_ce_selective_bwd": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, c_float, P, P, P, P, P]),
+    "selunet_ce_partials": (c_int32, [P, P, c_int64, c_int32, c_int64, P, P]),
+    "selunet_ce_bwd": (c_int32, [P, P, c_int64, c_int32, c_int64, c_double, P, P, P]),
     "selunet_loss_slab_rows": (c_int64, [c_int64]),
     "selunet_selective_partials": (c_int32, [P, P, P, c_int64, P, P]),
     "selunet_selective_finalize": (c_int32, [P, c_double, c_float, c_float, P, P, P, P]),
@@ -196,7 +208,10 @@ class Plan:
         pos = []
         for i, a in enumerate(args):
             if isinstance(a, ctypes.Structure):
-                _check_struct(a, self._slot, name)
+                fields = _struct_slots(a, self._slot)
+                if fields:  # per-call buffers inside a descriptor: rebound in a copy at replay
+                    args[i] = _StructSlots(type(a).from_buffer_copy(a), fields)
+                    pos.append(i)
                 continue
             sl = self._slot(a)
             if sl is not None:
@@ -218,24 +233,54 @@ class Plan:
             if pos:
                 a = list(args)
                 for i in pos:
-                    a[i] = base[a[i].name] + a[i].offset
+                    a[i] = a[i].bind(base) if isinstance(a[i], _StructSlots) else base[a[i].name] + a[i].offset
                 args = a
             rc = fn(*args) if _HOOK is None else _HOOK(name, args, lambda fn=fn, args=args: fn(*args))
             if rc != 0:
                 raise SelunetError(f"{name}: {L.selunet_last_error().decode()}")
 
 
-def _check_struct(st, slot_of, name):
+def _struct_slots(st, slot_of, path=()):
+    """(field path, Slot) of every pointer field of a (nested) descriptor that points into a
+    registered per-call buffer; a path step is a field name or (array field, index)."""
+    out = []
     for f, _ in st._fields_:
         v = getattr(st, f)
         if isinstance(v, ctypes.Structure):
-            _check_struct(v, slot_of, name)
+            out += _struct_slots(v, slot_of, path + (f,))
         elif isinstance(v, ctypes.Array):
-            for e in v:
+            for i, e in enumerate(v):
                 if isinstance(e, ctypes.Structure):
-                    _check_struct(e, slot_of, name)
-        elif slot_of(v) is not None:
-            raise RuntimeError(f"{name}: a per-call buffer is referenced inside a descriptor; it cannot be replayed")
+                    out += _struct_slots(e, slot_of, path + ((f, i),))
+                else:
+                    sl = slot_of(e)
+                    if sl is not None:
+                        out.append((path + ((f, i),), sl))
+        else:
+            sl = slot_of(v)
+            if sl is not None:
+                out.append((path + (f,), sl))
+    return out
+
+
+class _StructSlots:
+    """A recorded descriptor whose pointer fields into per-call buffers are rebound per replay."""
+
+    def __init__(self, st, fields):
+        self.st, self.fields = st, fields
+
+    def bind(self, base):
+        st = type(self.st).from_buffer_copy(self.st)
+        for path, sl in self.fields:
+            obj = st
+            for step in path[:-1]:
+                obj = getattr(obj, step[0])[step[1]] if isinstance(step, tuple) else getattr(obj, step)
+            last, v = path[-1], base[sl.name] + sl.offset
+            if isinstance(last, tuple):
+                getattr(obj, last[0])[last[1]] = v
+            else:
+                setattr(obj, last, v)
+        return st
 
 
 _REC = None

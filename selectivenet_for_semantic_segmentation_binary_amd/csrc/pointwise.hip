@@ -662,6 +662,226 @@ __global__ void bce_bwd_kernel(const float* __restrict__ a, const float* __restr
     d[i] = g * (sigmoidf_(a[i]) - t[i]) * inv_p;
 }
 
+// =========================================================================== N-output heads
+// The CE UNet's heads (model.py:170,174-175; 2 + 2 + 2 outputs for n_cls = 2) on relu(bn(y)):
+// 16 lanes per pixel (4 channels each), one 16-lane shuffle reduction per output. Outputs go to
+// per-output planes with an image stride, so NCHW logits are written in place.
+struct HeadPlanesArg {
+  int n, hw;
+  float* plane[8];
+  int64_t img_stride[8];
+  int w_off[8], b_off[8];
+  int row_len;
+};
+
+template <typename T>
+__global__ void heads_n_fwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                   const float* __restrict__ shift, const float* __restrict__ w,
+                                   const float* __restrict__ b, HeadPlanesArg hp) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+  f32x4 wv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) wv[k] = k < hp.n ? *reinterpret_cast<const f32x4*>(w + k * 64 + c) : f32x4{0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 4);
+  for (int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4); p < m; p += stride) {
+    f32x4 z = Vec4<T>::load(y + p * 64 + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = fmaxf(z[e] * sc[e] + sh[e], 0.0f);
+    const int64_t img = p / hp.hw, q = p - img * hp.hw;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < hp.n) {
+        float a = z[0] * wv[k][0] + z[1] * wv[k][1] + z[2] * wv[k][2] + z[3] * wv[k][3];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 16);
+        if (sub == 0) hp.plane[k][img * hp.img_stride[k] + q] = a + b[k];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void heads_n_bwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                   const float* __restrict__ shift, const float* __restrict__ w, HeadPlanesArg hp,
+                                   T* __restrict__ dz, float* slab, const float* __restrict__ mean,
+                                   const float* __restrict__ invstd, float* bn_slab) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+  const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+  f32x4 wv[8], dw[8];
+  float db[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wv[k] = k < hp.n ? *reinterpret_cast<const f32x4*>(w + k * 64 + c) : f32x4{0, 0, 0, 0};
+    dw[k] = f32x4{0, 0, 0, 0};
+    db[k] = 0.0f;
+  }
+  f32x4 mu = f32x4{0, 0, 0, 0}, is = f32x4{0, 0, 0, 0};
+  if (bn_slab) {
+    mu = *reinterpret_cast<const f32x4*>(mean + c);
+    is = *reinterpret_cast<const f32x4*>(invstd + c);
+  }
+  BnbAcc bn;
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (m + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(m, p0 + chunk);
+  for (int64_t p = p0 + (threadIdx.x >> 4); p < p1; p += (TPB >> 4)) {
+    const f32x4 yv = Vec4<T>::load(y + p * 64 + c);
+    f32x4 z;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = fmaxf(yv[e] * sc[e] + sh[e], 0.0f);
+    const int64_t img = p / hp.hw, q = p - img * hp.hw;
+    f32x4 d = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < hp.n) {
+        const float g = hp.plane[k][img * hp.img_stride[k] + q];
+        d += wv[k] * g;
+        dw[k] += z * g;
+        db[k] += g;
+      }
+    }
+    Vec4<T>::store(dz + p * 64 + c, d);
+    if (bn_slab) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<T>(d[e]));  // as stored
+      bn.add(yv, d, sc, sh, mu, is);
+    }
+  }
+  // block reduce: the 16 pixel lanes of each channel group, then the weight/bias sums per output
+  __shared__ f32x4 red[TPB];
+  __shared__ float redb[TPB];
+  float* row = slab + (int64_t)blockIdx.x * hp.row_len;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k < hp.n) {  // (block-uniform)
+      red[threadIdx.x] = dw[k];
+      redb[threadIdx.x] = sub == 0 ? db[k] : 0.0f;  // each pixel's g is carried by its sub == 0 lane
+      __syncthreads();
+      if (threadIdx.x < 16) {
+        f32x4 s = f32x4{0, 0, 0, 0};
+        for (int q = 0; q < TPB / 16; ++q) s += red[q * 16 + threadIdx.x];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) row[hp.w_off[k] + threadIdx.x * 4 + e] = s[e];  // (any offset)
+      }
+      if (threadIdx.x == 16) {
+        float s = 0.0f;
+        for (int q = 0; q < TPB; q += 16) s += redb[q];
+        row[hp.b_off[k]] = s;
+      }
+      __syncthreads();
+    }
+  }
+  if (bn_slab) channel_block_reduce<3>(bn.acc, 64, bn_slab + (int64_t)blockIdx.x * 3 * 64);
+}
+
+// =========================================================================== cross-entropy losses
+// logits NCHW [N][C][hw]; lse over C <= 8 classes (max-shifted), ell = lse - x[t]
+__device__ __forceinline__ float ce_pixel(const float* __restrict__ x, int64_t base, int64_t hw, int C, int t,
+                                          float (&e)[8], float& inv_se) {
+  float xv[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    xv[c] = c < C ? x[base + c * hw] : -INFINITY;
+    mx = fmaxf(mx, xv[c]);
+  }
+  float se = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    e[c] = c < C ? __expf(xv[c] - mx) : 0.0f;
+    se += e[c];
+  }
+  inv_se = 1.0f / se;
+  float xt = xv[0];
+#pragma unroll
+  for (int c = 1; c < 8; ++c) xt = c == t ? xv[c] : xt;
+  return mx + __logf(se) - xt;
+}
+
+__device__ __forceinline__ int ce_target(const int64_t* tgt, int64_t i, int C) {
+  const int64_t t = tgt[i];
+  return (int)(t < 0 ? 0 : (t >= C ? C - 1 : t));
+}
+
+__global__ void ce_selective_partials_kernel(const float* __restrict__ out, const float* __restrict__ sel,
+                                             const int64_t* __restrict__ tgt, int64_t P, int C, int64_t hw,
+                                             float* slab) {
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (P + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(P, p0 + chunk);
+  float acc[2] = {0.0f, 0.0f};
+  for (int64_t i = p0 + threadIdx.x; i < p1; i += TPB) {
+    const int64_t img = i / hw, q = i - img * hw;
+    const float s = sigmoidf_(sel[(img * 2 + 1) * hw + q] - sel[img * 2 * hw + q]);  // softmax(.)[:, 1]
+    float e[8], inv_se;
+    const float ell = ce_pixel(out, img * C * hw + q, hw, C, ce_target(tgt, i, C), e, inv_se);
+    acc[0] += s;
+    acc[1] += ell * s;
+  }
+  block_sum_store<2>(acc, slab + blockIdx.x * 2);
+}
+
+__global__ void ce_selective_bwd_kernel(const float* __restrict__ out, const float* __restrict__ sel,
+                                        const int64_t* __restrict__ tgt, int64_t P, int C, int64_t hw,
+                                        const float* state, float lamb, const float* g_loss, const float* g_cov,
+                                        float* d_out, float* d_sel) {
+  const float S0 = state[0], R = state[1], d = state[2], Pg = state[3];
+  const float gl = g_loss ? g_loss[0] : 1.0f;
+  const float gc = g_cov ? g_cov[0] : 0.0f;
+  const float inv_s0 = 1.0f / S0;
+  const float cterm = (gc - gl * 2.0f * lamb * d) / Pg;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i / hw, q = i - img * hw;
+    const int64_t s0i = img * 2 * hw + q, s1i = s0i + hw;
+    const float s = sigmoidf_(sel[s1i] - sel[s0i]);
+    const int t = ce_target(tgt, i, C);
+    const int64_t base = img * C * hw + q;
+    float e[8], inv_se;
+    const float ell = ce_pixel(out, base, hw, C, t, e, inv_se);
+    const float k = gl * s * inv_s0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < C) d_out[base + c * hw] = k * (e[c] * inv_se - (c == t ? 1.0f : 0.0f));
+    const float ds = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
+    d_sel[s1i] = ds;
+    d_sel[s0i] = -ds;
+  }
+}
+
+__global__ void ce_partials_kernel(const float* __restrict__ a, const int64_t* __restrict__ tgt, int64_t P, int C,
+                                   int64_t hw, float* slab) {
+  const int64_t rows = gridDim.x;
+  const int64_t chunk = (P + rows - 1) / rows;
+  const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(P, p0 + chunk);
+  float acc[1] = {0.0f};
+  for (int64_t i = p0 + threadIdx.x; i < p1; i += TPB) {
+    const int64_t img = i / hw, q = i - img * hw;
+    float e[8], inv_se;
+    acc[0] += ce_pixel(a, img * C * hw + q, hw, C, ce_target(tgt, i, C), e, inv_se);
+  }
+  block_sum_store<1>(acc, slab + blockIdx.x);
+}
+
+__global__ void ce_bwd_kernel(const float* __restrict__ a, const int64_t* __restrict__ tgt, int64_t P, int C,
+                              int64_t hw, float inv_p, const float* g_loss, float* d) {
+  const float g = (g_loss ? g_loss[0] : 1.0f) * inv_p;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i / hw, q = i - img * hw;
+    const int64_t base = img * C * hw + q;
+    const int t = ce_target(tgt, i, C);
+    float e[8], inv_se;
+    ce_pixel(a, base, hw, C, t, e, inv_se);
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < C) d[base + c * hw] = g * (e[c] * inv_se - (c == t ? 1.0f : 0.0f));
+  }
+}
+
 // =========================================================================== Adam
 __global__ void adam_kernel(const selunet_adam_tensor* __restrict__ list, int n, float lr_bc1, float beta1,
                             float beta2, float eps, float wd, float bc2_sqrt) {
@@ -957,6 +1177,99 @@ int selunet_adam_step(const selunet_adam_tensor* list, int32_t n, int64_t total_
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)total_chunks), dim3(TPB), 0, as_stream(stream), list, n,
                      (float)(lr / bc1), beta1, beta2, eps, weight_decay, (float)std::sqrt(bc2));
   return check_launch("adam_step");
+}
+
+static int head_planes_arg(const selunet_head_planes* a, HeadPlanesArg& h, bool bwd) {
+  SELUNET_REQUIRE(a != nullptr && a->n >= 1 && a->n <= 8 && a->hw > 0, "head planes: need 1..8 outputs and hw > 0");
+  std::memset(&h, 0, sizeof(h));
+  h.n = a->n;
+  h.hw = a->hw;
+  h.row_len = a->row_len;
+  for (int k = 0; k < a->n; ++k) {
+    SELUNET_REQUIRE(a->plane[k] != nullptr && a->img_stride[k] >= a->hw, "head planes: plane %d missing/bad stride", k);
+    h.plane[k] = a->plane[k];
+    h.img_stride[k] = a->img_stride[k];
+    h.w_off[k] = a->w_off[k];
+    h.b_off[k] = a->b_off[k];
+    if (bwd)
+      SELUNET_REQUIRE(a->w_off[k] >= 0 && a->w_off[k] + 64 <= a->row_len && a->b_off[k] >= 0 &&
+                          a->b_off[k] < a->row_len,
+                      "head planes: slab offsets of output %d outside row_len %d", k, a->row_len);
+  }
+  return 0;
+}
+
+int selunet_heads_fwd_planes(const void* y, int64_t m, const float* scale, const float* shift, const float* w,
+                             const float* b, const selunet_head_planes* out, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && w && b && m > 0, "heads_fwd_planes: bad arguments");
+  HeadPlanesArg h;
+  if (int rc = head_planes_arg(out, h, false)) return rc;
+  SELUNET_REQUIRE(m % h.hw == 0, "heads_fwd_planes: m (%lld) must be a multiple of hw (%d)", (long long)m, h.hw);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(heads_n_fwd_kernel<T>, dim3(grid_for(m * 16, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, w, b, h));
+  return check_launch("heads_fwd_planes");
+}
+
+int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const float* shift, const float* w,
+                             const selunet_head_planes* grads, void* dz, float* slab, const selunet_bn_bwd_stats* bnb,
+                             int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && w && dz && slab && m > 0, "heads_bwd_planes: bad arguments");
+  HeadPlanesArg h;
+  if (int rc = head_planes_arg(grads, h, true)) return rc;
+  SELUNET_REQUIRE(m % h.hw == 0, "heads_bwd_planes: m (%lld) must be a multiple of hw (%d)", (long long)m, h.hw);
+  const float *mean = nullptr, *invstd = nullptr;
+  float* bslab = nullptr;
+  if (bnb && bnb->slab) {
+    SELUNET_REQUIRE(bnb->y == y && bnb->scale == scale && bnb->shift == shift && bnb->mean && bnb->invstd,
+                    "heads_bwd_planes: bnb must describe the heads' input layer (same y/scale/shift)");
+    mean = bnb->mean;
+    invstd = bnb->invstd;
+    bslab = bnb->slab;
+  }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(heads_n_bwd_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, w, h, (T*)dz, slab, mean,
+                                       invstd, bslab));
+  return check_launch("heads_bwd_planes");
+}
+
+int selunet_ce_selective_partials(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                                  int64_t hw, float* slab, void* stream) {
+  SELUNET_REQUIRE(out && sel && target && slab && n > 0 && hw > 0 && c >= 1 && c <= 8,
+                  "ce_selective_partials: bad arguments (n_cls must be 1..8)");
+  const int64_t p = n * hw;
+  hipLaunchKernelGGL(ce_selective_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream),
+                     out, sel, target, p, c, hw, slab);
+  return check_launch("ce_selective_partials");
+}
+
+int selunet_ce_selective_bwd(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                             int64_t hw, const float* state, float lamb, const float* g_loss, const float* g_coverage,
+                             float* d_out, float* d_sel, void* stream) {
+  SELUNET_REQUIRE(out && sel && target && state && d_out && d_sel && n > 0 && hw > 0 && c >= 1 && c <= 8,
+                  "ce_selective_bwd: bad arguments");
+  const int64_t p = n * hw;
+  hipLaunchKernelGGL(ce_selective_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), out, sel,
+                     target, p, c, hw, state, lamb, g_loss, g_coverage, d_out, d_sel);
+  return check_launch("ce_selective_bwd");
+}
+
+int selunet_ce_partials(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw, float* slab,
+                        void* stream) {
+  SELUNET_REQUIRE(logit && target && slab && n > 0 && hw > 0 && c >= 1 && c <= 8, "ce_partials: bad arguments");
+  const int64_t p = n * hw;
+  hipLaunchKernelGGL(ce_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream), logit,
+                     target, p, c, hw, slab);
+  return check_launch("ce_partials");
+}
+
+int selunet_ce_bwd(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw, double p_global,
+                   const float* g_loss, float* d_logit, void* stream) {
+  SELUNET_REQUIRE(logit && target && d_logit && n > 0 && hw > 0 && c >= 1 && c <= 8 && p_global > 0,
+                  "ce_bwd: bad arguments");
+  const int64_t p = n * hw;
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), logit, target, p, c, hw,
+                     (float)(1.0 / p_global), g_loss, d_logit);
+  return check_launch("ce_bwd");
 }
 
 }  // extern "C"

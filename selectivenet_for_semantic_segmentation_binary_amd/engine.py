@@ -242,19 +242,25 @@ class Engine:
         if ctx is not None and ctx.entry is not None:
             ctx.entry.busy = False
 
-    def forward(self, x, P, B, selective, training, need_backward=False):
-        """x: [N, Cin, H, W] fp32 contiguous. Returns (heads tuple, ctx); the heads are new tensors."""
+    def forward(self, x, P, B, selective, training, need_backward=False, ce_heads=None):
+        """x: [N, Cin, H, W] fp32 contiguous. Returns (heads tuple, ctx); the heads are new tensors:
+        [N, H, W] logits for UNet_B, or, with ce_heads = [(head, channels)] (the CE `UNet`),
+        NCHW [N, channels, H, W] logits per head."""
         assert x.dim() == 4 and x.is_contiguous() and x.dtype == torch.float32
         n, cin, H, W = x.shape
         if H % 8 or W % 8:
             raise ValueError(f"UNet_B needs H and W divisible by 8 (three 2x2 poolings); got {H}x{W}")
-        nheads = 3 if selective else 1
-        outs = tuple(torch.empty(n, H, W, dtype=torch.float32, device=x.device) for _ in range(nheads))  # per call
-        e = self._entry_for(self._signature(x, P, B, selective, training, need_backward)) \
+        if ce_heads is None:
+            nheads = 3 if selective else 1
+            outs = tuple(torch.empty(n, H, W, dtype=torch.float32, device=x.device) for _ in range(nheads))
+        else:
+            ce_heads = tuple(ce_heads)
+            outs = tuple(torch.empty(n, c, H, W, dtype=torch.float32, device=x.device) for _, c in ce_heads)
+        e = self._entry_for(self._signature(x, P, B, selective, training, need_backward) + (ce_heads,)) \
             if self.plans_enabled else None
         slots = {"x": x, **{f"out{i}": o for i, o in enumerate(outs)}}
         if e is None:
-            ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs)
+            ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs, ce_heads)
         elif e.plan is not None:
             e.plan.replay(slots)
             ctx = e.ctx
@@ -262,16 +268,17 @@ class Engine:
         else:
             plan = K.Plan(slots)
             with K.recording(plan):
-                ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs)
+                ctx = self._forward_impl(x, P, B, selective, training, need_backward, outs, ce_heads)
             e.plan, e.ctx = plan, ctx
             ctx.entry = e
         if e is not None and training and need_backward:
             e.busy = True
         return outs, ctx
 
-    def _forward_impl(self, x, P, B, selective, training, need_backward, outs):
+    def _forward_impl(self, x, P, B, selective, training, need_backward, outs, ce_heads=None):
         n, cin, H, W = x.shape
         ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
+        ctx.ce_heads = ce_heads
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
         h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
@@ -297,6 +304,8 @@ class Engine:
         d12 = c("decoder_layer_1_2", h1, w1, K.source(u1, 64), e12.src())
         d11 = c("decoder_layer_1_1", h1, w1, d12.src())
         M = n * H * W
+        if ce_heads is not None:
+            return self._heads_fwd_planes(ctx, P, d11, outs, ce_heads, n, H * W)
         heads = LY.HEADS if selective else LY.HEADS[:1]
         hw = K.keep(torch.empty(len(heads), 64, dtype=torch.float32, device=x.device))
         hb = K.keep(torch.empty(len(heads), dtype=torch.float32, device=x.device))
@@ -307,6 +316,42 @@ class Engine:
         K.call("selunet_heads_fwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(hw), K.ptr(hb),
                len(heads), K.ptr(o[0]), K.ptr(o[1]), K.ptr(o[2]), self.code, self.stream)
         ctx.head_w = hw
+        return ctx
+
+    # ------------------------------------------------------------------ N-output heads (CE UNet)
+    @staticmethod
+    def _planes(tensors, ce_heads, hw, with_slab=False):
+        """selunet_head_planes over per-head NCHW tensors [N, c, H, W]; with_slab: the slab offsets of
+        each output's weight (64) and bias sums in the heads' segment of the gradient buffer
+        (registration order: weight [c, 64] then bias [c] per head)."""
+        d = K.HeadPlanes()
+        k, off = 0, 0
+        for t, (_, c) in zip(tensors, ce_heads):
+            for j in range(c):
+                d.plane[k] = t.data_ptr() + j * hw * 4
+                d.img_stride[k] = c * hw
+                d.w_off[k] = off + j * 64
+                d.b_off[k] = off + c * 64 + j
+                k += 1
+            off += c * 65
+        d.n, d.hw, d.row_len = k, hw, off
+        return d
+
+    def _heads_fwd_planes(self, ctx, P, d11, outs, ce_heads, n, hw):
+        no = sum(c for _, c in ce_heads)
+        if no > 8:
+            raise ValueError(f"the heads have {no} output channels; the MI355X heads kernel takes at most 8")
+        dev = d11.y.device
+        w = K.keep(torch.empty(no, 64, dtype=torch.float32, device=dev))
+        b = K.keep(torch.empty(no, dtype=torch.float32, device=dev))
+        k = 0
+        for h, c in ce_heads:  # the heads' current weights, gathered in stream order
+            K.call("selunet_memcpy", K.ptr(w[k:]), K.ptr(P[f"{h}.weight"]), c * 64 * 4, self.stream)
+            K.call("selunet_memcpy", K.ptr(b[k:]), K.ptr(P[f"{h}.bias"]), c * 4, self.stream)
+            k += c
+        K.call("selunet_heads_fwd_planes", K.ptr(d11.y), n * hw, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(w), K.ptr(b),
+               self._planes(outs, ce_heads, hw), self.code, self.stream)
+        ctx.head_w = w
         return ctx
 
     # ------------------------------------------------------------------ backward pieces
@@ -438,25 +483,42 @@ class Engine:
         dev = ctx.x.device
         bn = ctx.bn
         heads = LY.HEADS if ctx.selective else LY.HEADS[:1]
-        gs = [g if g is not None else K.keep(torch.zeros(n, H, W, dtype=torch.float32, device=dev)) for g in g_heads]
-        gs = gs + [None] * (3 - len(gs))
         d11 = bn["decoder_layer_1_1"]
         dz = K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
         rows = K.query("selunet_channel_slab_rows", M)
-        nh = len(heads)
-        slab = K.keep(torch.empty(rows, nh * 65, dtype=torch.float32, device=dev))
         bslab = K.keep(torch.empty(rows, 3, 64, dtype=torch.float32, device=dev))
-        K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
-               K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
-               self.stream)
+        ce = getattr(ctx, "ce_heads", None)
+        if ce is not None:
+            heads = [h for h, _ in ce]
+            gs = [g if g is not None else K.keep(torch.zeros(n, c, H, W, dtype=torch.float32, device=dev))
+                  for g, (_, c) in zip(g_heads, ce)]
+            planes = self._planes(gs, ce, H * W, with_slab=True)
+            slab = K.keep(torch.empty(rows, planes.row_len, dtype=torch.float32, device=dev))
+            K.call("selunet_heads_bwd_planes", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w),
+                   planes, K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code, self.stream)
+            seg = planes.row_len
+        else:
+            gs = [g if g is not None else K.keep(torch.zeros(n, H, W, dtype=torch.float32, device=dev))
+                  for g in g_heads]
+            gs = gs + [None] * (3 - len(gs))
+            nh = len(heads)
+            slab = K.keep(torch.empty(rows, nh * 65, dtype=torch.float32, device=dev))
+            K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
+                   K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
+                   self.stream)
+            seg = nh * 65
         dz = DGrad(dz, bslab, rows)
-        # head weight/bias grads are consecutive in the gradient buffer ([nh][64 + 1], registration
-        # order conv1x1, conv_select, conv_aux): reduce straight into it
+        # the head weight/bias grads are one consecutive segment of the gradient buffer (registration
+        # order conv1x1, conv_select, conv_aux; weight then bias each): reduce straight into it
         hw0 = G[f"{heads[0]}.weight"]
-        for i, h in enumerate(heads):
-            assert G[f"{h}.weight"].data_ptr() == hw0.data_ptr() + i * 65 * 4
-            assert G[f"{h}.bias"].data_ptr() == hw0.data_ptr() + (i * 65 + 64) * 4
-        self._reduce(slab, rows, nh * 65, out32=hw0)
+        off = 0
+        for h in heads:
+            assert G[f"{h}.weight"].data_ptr() == hw0.data_ptr() + off * 4
+            off += G[f"{h}.weight"].numel()
+            assert G[f"{h}.bias"].data_ptr() == hw0.data_ptr() + off * 4
+            off += G[f"{h}.bias"].numel()
+        assert off == seg
+        self._reduce(slab, rows, seg, out32=hw0)
         K.marker(("grads", "heads"))
 
         e12, e22, e32 = bn["encoder_layer_1_2"], bn["encoder_layer_2_2"], bn["encoder_layer_3_2"]

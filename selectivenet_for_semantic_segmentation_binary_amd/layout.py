@@ -55,8 +55,21 @@ def input_channels(input_type: str) -> int:
     raise ValueError(f"unsupported input_type {input_type!r} (reference accepts '*RGB*' or 'GH')")
 
 
-def param_specs(input_type: str = "RGB", selective: bool = False):
-    """Parameters in registration order: list of (key, shape, kind, fan_in).
+def head_channels(selective: bool, n_cls: int | None = None):
+    """[(head, output channels)] in registration order: UNet_B (n_cls None, model.py:62,65-66) has
+    1-channel heads; the CE UNet (model.py:170,174-175) conv1x1 -> n_cls, conv_select -> 2,
+    conv_aux -> n_cls."""
+    if n_cls is None:
+        ch = [1, 1, 1]
+    else:
+        ch = [n_cls, 2, n_cls]
+    heads = list(zip(HEADS, ch))
+    return heads if selective else heads[:1]
+
+
+def param_specs(input_type: str = "RGB", selective: bool = False, n_cls: int | None = None):
+    """Parameters in registration order: list of (key, shape, kind, fan_in). n_cls: None for
+    UNet_B, the class count for the CE `UNet` (model.py:106-191; only the heads differ).
 
     kind in {conv_w, conv_b, bn_w, bn_b, convT_w, convT_b, head_w, head_b}.
     fan_in follows torch.nn.init._calculate_fan_in_and_fan_out (dim 1 * k*k),
@@ -89,10 +102,9 @@ def param_specs(input_type: str = "RGB", selective: bool = False):
     unpool(*UNPOOLS[2])
     cbr("decoder_layer_1_2", *lay["decoder_layer_1_2"])
     cbr("decoder_layer_1_1", *lay["decoder_layer_1_1"])
-    heads = HEADS if selective else HEADS[:1]
-    for h in heads:
-        specs.append((f"{h}.weight", (1, 64, 1, 1), "head_w", 64))
-        specs.append((f"{h}.bias", (1,), "head_b", 64))
+    for h, c in head_channels(selective, n_cls):
+        specs.append((f"{h}.weight", (c, 64, 1, 1), "head_w", 64))
+        specs.append((f"{h}.bias", (c,), "head_b", 64))
     return specs
 
 
@@ -106,10 +118,10 @@ def buffer_specs():
     return out
 
 
-def state_dict_keys(input_type: str = "RGB", selective: bool = False):
-    """Exact key order of the reference `UNet_B(...).state_dict()`."""
+def state_dict_keys(input_type: str = "RGB", selective: bool = False, n_cls: int | None = None):
+    """Exact key order of the reference `UNet_B(...)` / `UNet(...)` `state_dict()`."""
     keys = []
-    for key, _, kind, _ in param_specs(input_type, selective):
+    for key, _, kind, _ in param_specs(input_type, selective, n_cls):
         keys.append(key)
         if kind == "bn_b":
             base = key[: -len(".bias")]
@@ -118,7 +130,7 @@ def state_dict_keys(input_type: str = "RGB", selective: bool = False):
 
 
 def seeded_params(seed: int = 0, input_type: str = "RGB", selective: bool = False,
-                  bn_affine_random: bool = True):
+                  bn_affine_random: bool = True, n_cls: int | None = None):
     """Deterministic parameter recipe (numpy PCG64), torch-default-like bounds.
 
     conv/convT/head weights and biases ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (the bound
@@ -128,7 +140,7 @@ def seeded_params(seed: int = 0, input_type: str = "RGB", selective: bool = Fals
     """
     rng = np.random.Generator(np.random.PCG64(seed))
     out = {}
-    for key, shape, kind, fan_in in param_specs(input_type, selective):
+    for key, shape, kind, fan_in in param_specs(input_type, selective, n_cls):
         if kind in ("bn_w",):
             v = rng.uniform(0.6, 1.4, size=shape) if bn_affine_random else np.ones(shape)
         elif kind in ("bn_b",):
@@ -140,5 +152,5 @@ def seeded_params(seed: int = 0, input_type: str = "RGB", selective: bool = Fals
     return out
 
 
-def count_params(input_type: str = "RGB", selective: bool = False) -> int:
-    return int(sum(np.prod(s) for _, s, _, _ in param_specs(input_type, selective)))
+def count_params(input_type: str = "RGB", selective: bool = False, n_cls: int | None = None) -> int:
+    return int(sum(np.prod(s) for _, s, _, _ in param_specs(input_type, selective, n_cls)))

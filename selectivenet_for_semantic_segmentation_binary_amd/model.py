@@ -96,7 +96,8 @@ class _UNetBFunction(torch.autograd.Function):
             parallel.broadcast_buffers(module)  # DataParallel replicas read device 0's buffers
         eng = module._engine()
         need_bwd = training and any(ctx.needs_input_grad[2:])
-        outs, ectx = eng.forward(x.contiguous(), P, B, module.selective, training, need_backward=need_bwd)
+        outs, ectx = eng.forward(x.contiguous(), P, B, module.selective, training, need_backward=need_bwd,
+                                 ce_heads=module._ce_heads)
         if need_bwd:
             ctx.ectx = ectx
             ctx.eng = eng
@@ -133,10 +134,11 @@ class _UNetBFunction(torch.autograd.Function):
         return (None, None, *[G[n] for n in names])
 
 
-class UNet_B(nn.Module):
-    """model.py:18-103 UNet for BCE loss, optionally SelectiveNet (selection + aux heads)."""
+class _UNetBase(nn.Module):
+    """The encoder-decoder shared by UNet_B (model.py:18-103) and the CE UNet (model.py:105-191);
+    they differ only in the 1x1 heads (n_cls None: 1-channel heads)."""
 
-    def __init__(self, input_type="RGB", selective=False, compute_dtype=torch.float32):
+    def __init__(self, input_type="RGB", selective=False, compute_dtype=torch.float32, n_cls=None):
         super().__init__()
         self.selective = selective
         input_ch = LY.input_channels(input_type)
@@ -162,10 +164,9 @@ class UNet_B(nn.Module):
         self.unpool1 = _ConvTranspose2dParams(128, 64, 2)
         self.decoder_layer_1_2 = CBR_2D(in_ch=128, out_ch=64)
         self.decoder_layer_1_1 = CBR_2D(in_ch=64, out_ch=64)
-        self.conv1x1 = _Conv2dParams(64, 1, 1)
-        if self.selective:
-            self.conv_select = _Conv2dParams(64, 1, 1)
-            self.conv_aux = _Conv2dParams(64, 1, 1)
+        for h, c in LY.head_channels(selective, n_cls):
+            setattr(self, h, _Conv2dParams(64, c, 1))
+        self._ce_heads = None if n_cls is None else LY.head_channels(selective, n_cls)
         self._param_names = [n for n, _ in self.named_parameters()]
         self._engines = {}
 
@@ -184,3 +185,24 @@ class UNet_B(nn.Module):
         if x.dtype != torch.float32:
             x = x.float()
         return _UNetBFunction.apply(x, self, *params)
+
+
+class UNet_B(_UNetBase):
+    """model.py:18-103 UNet for BCE loss, optionally SelectiveNet (selection + aux heads):
+    [N, C_in, H, W] -> (N, H, W) logits, or (out, select, aux) each (N, H, W)."""
+
+    def __init__(self, input_type="RGB", selective=False, compute_dtype=torch.float32):
+        super().__init__(input_type, selective, compute_dtype)
+
+
+class UNet(_UNetBase):
+    """model.py:105-191 UNet for CE loss: conv1x1 64 -> n_cls; when selective conv_select 64 -> 2 and
+    conv_aux 64 -> n_cls. [N, C_in, H, W] -> (N, n_cls, H, W) logits, or (out, select, aux) with
+    select (N, 2, H, W) (model.py:182-189). n_cls + 2 + n_cls <= 8 output channels (n_cls <= 3
+    selective, <= 8 otherwise) — the reference trains with n_cls = 2 (train.py:23)."""
+
+    def __init__(self, input_type="RGB", n_cls=2, selective=False, compute_dtype=torch.float32):
+        if n_cls < 1 or sum(c for _, c in LY.head_channels(selective, n_cls)) > 8:
+            raise ValueError(f"n_cls={n_cls}: the heads may have at most 8 output channels in total")
+        super().__init__(input_type, selective, compute_dtype, n_cls=n_cls)
+        self.n_cls = n_cls

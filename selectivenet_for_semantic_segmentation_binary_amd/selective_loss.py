@@ -151,3 +151,121 @@ class BCEWithLogitsLoss(nn.Module):
             raise ValueError(f"Target size ({tuple(target.shape)}) must be the same as input size "
                              f"({tuple(input.shape)})")
         return _BCEWithLogitsMean.apply(_check(input, "input"), _check(target, "target"))
+
+
+# ----------------------------------------------------------------------------- CE forms (CE UNet)
+def _check_target_ce(target, logits):
+    if target.device.type != "cuda":
+        raise RuntimeError("target must be a cuda tensor (the MI355X losses have no CPU fallback)")
+    if target.dtype != torch.int64:
+        raise RuntimeError(f"expected int64 class indices as target (got {target.dtype})")
+    n, c, h, w = logits.shape
+    if tuple(target.shape) != (n, h, w):
+        raise ValueError(f"target {tuple(target.shape)} must be (N, H, W) = {(n, h, w)} for logits "
+                         f"{tuple(logits.shape)}")
+    if c > 8:
+        raise ValueError(f"at most 8 classes on the MI355X path (got {c})")
+    return target.contiguous()
+
+
+class _SelectiveRiskCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, output, selection, target, target_coverage, lamb):
+        n, c, h, w = output.shape
+        hw, p = h * w, n * h * w
+        dev = output.device
+        rows = K.query("selunet_loss_slab_rows", p)
+        slab = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        K.call("selunet_ce_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, hw, K.ptr(slab),
+               K.stream_ptr())
+        sums = _reduced_sums(slab, rows, 2)
+        p_global = global_count((n, h, w))
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        coverage = torch.empty((), dtype=torch.float32, device=dev)
+        state = torch.empty(4, dtype=torch.float32, device=dev)
+        K.call("selunet_selective_finalize", K.ptr(sums), p_global, float(lamb), float(target_coverage), K.ptr(loss),
+               K.ptr(coverage), K.ptr(state), K.stream_ptr())
+        ctx.save_for_backward(output, selection, target, state)
+        ctx.lamb = float(lamb)
+        return loss, coverage
+
+    @staticmethod
+    def backward(ctx, g_loss, g_cov):
+        output, selection, target, state = ctx.saved_tensors
+        n, c, h, w = output.shape
+        d_out = torch.empty_like(output)
+        d_sel = torch.empty_like(selection)
+        gl = g_loss.contiguous().float() if g_loss is not None else None
+        gc = g_cov.contiguous().float() if g_cov is not None else None
+        K.call("selunet_ce_selective_bwd", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, h * w, K.ptr(state),
+               ctx.lamb, K.ptr(gl), K.ptr(gc), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
+        return d_out, d_sel, None, None, None
+
+
+def calc_selective_risk_image(output, selection, target, target_coverage=0.8, lamb=8, hard_selection=False):
+    """selective_loss.py:24-56 (cross-entropy selective risk, CE `UNet`): output (N, C, H, W),
+    selection (N, 2, H, W), target (N, H, W) int64 class indices.
+
+        s = softmax(selection, 1)[:, 1]; coverage = mean(s)
+        risk = -mean(sum_c log_softmax(output, 1) * onehot(target) * s) / coverage
+        loss = risk + lamb * max(target_coverage - coverage, 0)^2
+
+    (the reference's one-hot target (N, C, H, W) form is accepted too and reduced to indices)."""
+    if hard_selection:
+        raise NotImplementedError("hard_selection=True (selective_loss.py:43-48) is not on the training path "
+                                  "and is not implemented on the MI355X path")
+    if output.dim() != 4 or selection.dim() != 4 or selection.shape[1] != 2 or \
+            selection.shape[0] != output.shape[0] or selection.shape[2:] != output.shape[2:]:
+        raise ValueError(f"expected output (N, C, H, W) and selection (N, 2, H, W); got {tuple(output.shape)}, "
+                         f"{tuple(selection.shape)}")
+    if target.dim() == 4:  # one-hot (N, C, H, W) as selective_loss.py:36-37 builds it
+        target = target.argmax(1)
+    o, s = _check(output, "output"), _check(selection, "selection")
+    return _SelectiveRiskCE.apply(o, s, _check_target_ce(target, o), target_coverage, lamb)
+
+
+class _CrossEntropyMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logit, target):
+        n, c, h, w = logit.shape
+        p = n * h * w
+        dev = logit.device
+        rows = K.query("selunet_loss_slab_rows", p)
+        slab = torch.empty(rows, 1, dtype=torch.float32, device=dev)
+        K.call("selunet_ce_partials", K.ptr(logit), K.ptr(target), n, c, h * w, K.ptr(slab), K.stream_ptr())
+        sums = _reduced_sums(slab, rows, 1)
+        p_global = global_count((n, h, w))
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        K.call("selunet_bce_finalize", K.ptr(sums), p_global, K.ptr(loss), K.stream_ptr())
+        ctx.save_for_backward(logit, target)
+        ctx.p_global = p_global
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logit, target = ctx.saved_tensors
+        n, c, h, w = logit.shape
+        d = torch.empty_like(logit)
+        g = g.contiguous().float()
+        K.call("selunet_ce_bwd", K.ptr(logit), K.ptr(target), n, c, h * w, ctx.p_global, K.ptr(g), K.ptr(d),
+               K.stream_ptr())
+        return d, None
+
+
+class CrossEntropyLoss(nn.Module):
+    """torch.nn.CrossEntropyLoss() with the defaults the reference uses (train.py:80): mean over
+    pixels, (N, C, H, W) logits, (N, H, W) int64 targets, no weights / ignore_index / smoothing."""
+
+    def __init__(self, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean",
+                 label_smoothing=0.0):
+        super().__init__()
+        if weight is not None or size_average is not None or reduce is not None or reduction != "mean" \
+                or label_smoothing != 0.0:
+            raise NotImplementedError("only the reference's CrossEntropyLoss() (mean, unweighted) is implemented")
+        self.ignore_index = ignore_index
+
+    def forward(self, input, target):
+        if input.dim() != 4:
+            raise ValueError(f"expected (N, C, H, W) logits, got {tuple(input.shape)}")
+        t = _check_target_ce(target, input)
+        return _CrossEntropyMean.apply(_check(input, "input"), t)

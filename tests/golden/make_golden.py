@@ -389,9 +389,86 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
           f"(selective {out['val_miou_selective']:.4f}), val selected {vsel}/{n_val * size * size}")
 
 
+def build_ref_ce(seed, selective, n_cls=2, input_type="RGB"):
+    """The reference's CE `UNet` (model.py:106-191) with the build's seeded weights."""
+    net = ref_model.UNet(input_type, n_cls, selective=selective)
+    sd = net.state_dict()
+    p = L.seeded_params(seed, input_type, selective, n_cls=n_cls)
+    assert list(sd.keys()) == L.state_dict_keys(input_type, selective, n_cls=n_cls), "state_dict key order drift"
+    net.load_state_dict(OrderedDict((k, torch.tensor(p[k]) if k in p else v) for k, v in sd.items()))
+    return net
+
+
+def ref_step_ce(net, optim, x, lab, selective, lamb):
+    """train.py:186-209 with --loss CE --model_arch UNet: CrossEntropyLoss aux + calc_selective_risk_image."""
+    loss_A = torch.nn.CrossEntropyLoss()
+    res = {}
+    if selective:
+        output, selection, aux = net(x)
+        aux_loss = loss_A(aux, lab)
+        select_loss, coverage = ref_loss.calc_selective_risk_image(output, selection, target=lab, lamb=lamb)
+        loss = aux_loss + select_loss
+        res.update(selection=selection.detach(), aux=aux.detach(), aux_loss=aux_loss.detach(),
+                   select_loss=select_loss.detach(), coverage=coverage.detach())
+    else:
+        output = net(x)
+        loss = loss_A(output, lab)
+    optim.zero_grad()
+    loss.backward()
+    grads = OrderedDict((n, p.grad.detach().clone()) for n, p in net.named_parameters())
+    optim.step()
+    res.update(output=output.detach(), loss=loss.detach(), grads=grads)
+    return res
+
+
+def ce_step_fixture(fname, n, size, selective, lamb=2, steps=2, seed=0, data_seed=5, n_cls=2):
+    """The CE UNet training iteration (fp32 steps + the fp64 step-0 truth); labels int64."""
+    x, lab = make_batch(n, size, seed=data_seed)
+    lab64 = lab.astype(np.int64)
+    out = {"meta_n": n, "meta_size": size, "meta_selective": int(selective), "meta_lamb": lamb,
+           "meta_steps": steps, "meta_seed": seed, "meta_data_seed": data_seed, "meta_n_cls": n_cls,
+           "x": x, "label": lab64}
+    torch.manual_seed(0)
+    net = build_ref_ce(seed, selective, n_cls)
+    net.train()
+    optim = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=0)
+    for s in range(steps):
+        r = ref_step_ce(net, optim, torch.tensor(x), torch.tensor(lab64), selective, lamb)
+        pre = f"s{s}/"
+        for k in ("loss", "aux_loss", "select_loss", "coverage"):
+            if k in r:
+                out[pre + k] = np.float64(r[k].item())
+        for h in ["output"] + (["selection", "aux"] if selective else []):
+            out[pre + h] = r[h].numpy().astype(np.float32)
+        record_tensors(out, pre + "grad", r["grads"])
+        record_tensors(out, pre + "param", OrderedDict(net.named_parameters()))
+        for k, v in net.state_dict().items():
+            if "running" in k:
+                out[pre + "buf/" + k] = v.numpy().astype(np.float32)
+    net = build_ref_ce(seed, selective, n_cls).double()
+    net.train()
+    optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+    r = ref_step_ce(net, optim, torch.tensor(x, dtype=torch.float64), torch.tensor(lab64), selective, lamb)
+    out["s0/loss64"] = np.float64(r["loss"].item())
+    for k, t in r["grads"].items():
+        a = t.numpy().astype(np.float64).ravel()
+        out[f"s0/grad64norm/{k}"] = np.float64(np.linalg.norm(a))
+        if f"s0/gradfull/{k}" in out:
+            out[f"s0/grad64full/{k}"] = a
+        else:
+            out[f"s0/grad64val/{k}"] = a[out[f"s0/gradidx/{k}"]]
+    path = os.path.join(HERE, fname)
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB): loss {out['s0/loss']:.6f}")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["miou"]:
         miou_fixture()
+        sys.exit(0)
+    if sys.argv[1:] == ["ce"]:
+        ce_step_fixture("step_ce_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
+        ce_step_fixture("step_ce_nosel_n2_32.npz", 2, 32, selective=False, steps=1)
         sys.exit(0)
     kats()
     loss_cases()
@@ -402,3 +479,5 @@ if __name__ == "__main__":
     step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=True)
     eval_fixture("eval_sel_n4_64.npz")
     miou_fixture()
+    ce_step_fixture("step_ce_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
+    ce_step_fixture("step_ce_nosel_n2_32.npz", 2, 32, selective=False, steps=1)

@@ -1,0 +1,119 @@
+"""The CE UNet variant (model.py:106-191) on the MI355X path: `UNet(input_type, n_cls, selective)`
+with `calc_selective_risk_image` (selective_loss.py:24-56) and `CrossEntropyLoss` (train.py:80),
+against the reference's own training step (tests/golden/step_ce_*.npz, written by
+tests/golden/make_golden.py from the reference model/loss) and against torch fp32 on the CPU for
+the loss kernels. Tolerances as for UNet_B (tests/test_gpu_model.py): step 0 loss / coverage /
+logits 1e-4 relative, argmax masks bit-exact away from ties, gradients vs the reference's fp64 run
+no worse than max(3 x its fp32 error, 1e-2); the second step loosely (Adam amplifies rounding of
+near-zero gradients).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import selectivenet_for_semantic_segmentation_binary_amd as S
+import selectivenet_for_semantic_segmentation_binary_amd.layout as L
+from oracle import unet_b_cpu as O
+from tests import _golden as G
+from tests.test_gpu_model import PRE_BN_BIAS
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def build_ce(selective, n_cls=2, seed=0, dtype=torch.float32):
+    net = S.UNet("RGB", n_cls, selective=selective, compute_dtype=dtype)
+    p = L.seeded_params(seed, "RGB", selective, n_cls=n_cls)
+    assert list(net.state_dict().keys()) == L.state_dict_keys("RGB", selective, n_cls=n_cls)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    return net.to(DEV).train()
+
+
+def ce_step(net, opt, x, lab, selective, lamb):
+    loss_A = S.CrossEntropyLoss()
+    res = {}
+    if selective:
+        out, sel, aux = net(x)
+        aux_loss = loss_A(aux, lab)
+        select_loss, coverage = S.calc_selective_risk_image(out, sel, target=lab, lamb=lamb)
+        loss = aux_loss + select_loss
+        res.update(coverage=coverage.item(), aux_loss=aux_loss.item(), select_loss=select_loss.item(),
+                   selection=sel.detach().cpu().numpy())
+    else:
+        out = net(x)
+        loss = loss_A(out, lab)
+    opt.zero_grad()
+    loss.backward()
+    res["grads"] = {k: p.grad.detach().cpu().numpy().copy() for k, p in net.named_parameters()}
+    opt.step()
+    res.update(loss=loss.item(), output=out.detach().cpu().numpy())
+    return res
+
+
+@pytest.mark.parametrize("fname", ["step_ce_sel_n2_64.npz", "step_ce_nosel_n2_32.npz"])
+def test_ce_unet_step_matches_reference(fname):
+    d = G.load(fname)
+    selective, lamb = bool(d["meta_selective"]), int(d["meta_lamb"])
+    net = build_ce(selective, int(d["meta_n_cls"]), int(d["meta_seed"]))
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    x, lab = torch.tensor(d["x"], device=DEV), torch.tensor(d["label"], device=DEV)
+    for s in range(int(d["meta_steps"])):
+        r = ce_step(net, opt, x, lab, selective, lamb)
+        pre = f"s{s}/"
+        tol = 1e-4 if s == 0 else 1e-2
+        ref_loss = float(d[pre + "loss"])
+        assert abs(r["loss"] - ref_loss) < tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
+        if selective:
+            assert abs(r["coverage"] - float(d[pre + "coverage"])) < tol
+            assert G.max_rel(r["selection"], d[pre + "selection"]) < (1e-4 if s == 0 else 5e-2)
+        assert G.max_rel(r["output"], d[pre + "output"]) < (1e-4 if s == 0 else 5e-2)
+        if s == 0:
+            ref = d[pre + "output"]
+            pred, ref_pred = r["output"].argmax(1), ref.argmax(1)
+            srt = np.sort(ref, axis=1)
+            tie = (srt[:, -1] - srt[:, -2]) < 1e-4 * np.abs(ref).max()
+            assert np.array_equal(pred[~tie], ref_pred[~tie])
+            fails, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
+            assert not fails, "\n".join(fails[:10])
+
+
+@pytest.mark.parametrize("n,c,h,w", [(2, 2, 16, 24), (3, 3, 8, 8), (1, 5, 16, 16)])
+def test_ce_loss_kernels_against_torch(n, c, h, w):
+    """calc_selective_risk_image / CrossEntropyLoss forward and gradients vs torch fp32 (CPU)."""
+    g = torch.Generator().manual_seed(7)
+    out = torch.randn(n, c, h, w, generator=g) * 3
+    sel = torch.randn(n, 2, h, w, generator=g) * 2
+    aux = torch.randn(n, c, h, w, generator=g) * 3
+    lab = torch.randint(0, c, (n, h, w), generator=g)
+    oc, sc, ac = (t.clone().requires_grad_() for t in (out, sel, aux))
+    l_ref, cov_ref = O.selective_risk_ce_literal(oc, sc, lab, lamb=8)
+    l_ref = l_ref + O.ce_mean(ac, lab)
+    l_ref.backward()
+    og, sg, ag = (t.to(DEV).requires_grad_() for t in (out, sel, aux))
+    l, cov = S.calc_selective_risk_image(og, sg, lab.to(DEV), lamb=8)
+    l = l + S.CrossEntropyLoss()(ag, lab.to(DEV))
+    l.backward()
+    assert abs(l.item() - l_ref.item()) < 1e-5 * max(1.0, abs(l_ref.item()))
+    assert abs(cov.item() - cov_ref.item()) < 1e-6
+    for a, b in ((og, oc), (sg, sc), (ag, ac)):
+        assert G.max_rel(a.grad.cpu().numpy(), b.grad.numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("n_cls,selective", [(3, False), (2, True)])
+def test_ce_unet_forward_bf16_and_classes(n_cls, selective):
+    """Other class counts / bf16 through the N-output heads kernel vs the oracle (fp32 logits within
+    1e-4 relative; bf16 within 3e-2)."""
+    x = torch.randn(2, 3, 32, 32, generator=torch.Generator().manual_seed(3))
+    params, buffers = O.make_state(1, "RGB", selective, n_cls=n_cls)
+    ref = O.forward(params, buffers, x, selective, training=True, ce=True)
+    ref = ref if selective else (ref,)
+    for dt, tol in ((torch.float32, 1e-4), (torch.bfloat16, 3e-2)):
+        net = build_ce(selective, n_cls, seed=1, dtype=dt)
+        got = net(x.to(DEV))
+        got = got if selective else (got,)
+        for a, b in zip(got, ref):
+            assert tuple(a.shape) == tuple(b.shape)
+            assert G.max_rel(a.detach().cpu().numpy(), b.detach().numpy()) < tol

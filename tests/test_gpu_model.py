@@ -253,7 +253,7 @@ def test_step_against_oracle_shapes(input_type, n, h, w, selective):
         else:
             l2 = O.bce_with_logits_mean(ro, lo)
         l2.backward()
-        return float(l2), {k: v.grad.double() for k, v in params.items()}
+        return float(l2.detach()), {k: v.grad.double() for k, v in params.items()}
 
     loss32, g32 = oracle(torch.float32)
     _, g64 = oracle(torch.float64)

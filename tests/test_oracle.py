@@ -161,3 +161,34 @@ def test_oracle_eval_forward():
     cm = O.confusion_matrix(d["label"].astype("uint8"), pred, selection=O.eval_pred_mask(s.numpy()))
     assert np.array_equal(cm, d["eval_cm_selective"])
     assert abs(O.miou(cm) - float(d["eval_miou_selective"])) < 1e-12
+
+
+def _oracle_ce_step(d, params, buffers):
+    selective = bool(d["meta_selective"])
+    x, lab = torch.tensor(d["x"]), torch.tensor(d["label"])
+    r = O.forward(params, buffers, x, selective, training=True, ce=True)
+    if selective:
+        o, s, a = r
+        sl, cov = O.selective_risk_ce_literal(o, s, lab, lamb=int(d["meta_lamb"]))
+        loss = O.ce_mean(a, lab) + sl
+    else:
+        o, cov, loss = r, None, O.ce_mean(r, lab)
+    loss.backward()
+    return o, cov, loss
+
+
+@pytest.mark.parametrize("fname", ["step_ce_sel_n2_64.npz", "step_ce_nosel_n2_32.npz"])
+def test_oracle_ce_unet_step_matches_reference(fname):
+    """The CE UNet (model.py:106-191) + calc_selective_risk_image (selective_loss.py:24-56) +
+    CrossEntropyLoss restated in the oracle, pinned to the reference's own run of the step."""
+    d = G.load(fname)
+    selective = bool(d["meta_selective"])
+    params, buffers = O.make_state(int(d["meta_seed"]), "RGB", selective, n_cls=int(d["meta_n_cls"]))
+    o, cov, loss = _oracle_ce_step(d, params, buffers)
+    assert abs(loss.item() - float(d["s0/loss"])) < 1e-5
+    if selective:
+        assert abs(cov.item() - float(d["s0/coverage"])) < 1e-6
+    assert G.max_rel(o.detach().numpy(), d["s0/output"]) < 1e-5
+    grads = {k: v.grad.numpy() for k, v in params.items()}
+    fails = G.check_tensors(d, "s0/grad", grads, rtol=1e-4, atol=0.0, atol_by_name={k: 1e-6 for k in PRE_BN_BIAS})
+    assert not fails, "\n".join(fails[:20])
