@@ -45,6 +45,11 @@ def logit_threshold(rule: str = "train", cut_off: float = 0.5, output_scale: str
     rule 'eval':  eval.py:171,175,229-231 — fn_sigmoid on the float32 array, `> cut_off`.
     output_scale != 'sigmoid': the raw logit is compared (`> cut_off`).
     """
+    if rule == "argmax":
+        # CE UNet with 2 classes (train.py:207-209, 216-219: np.argmax over the class / selection
+        # axis, ties -> class 0): callers pass the fp32 difference x1 - x0, which is > 0 exactly
+        # when x1 > x0; the smallest positive fp32 makes `>= t` the strict comparison.
+        return float(np.nextafter(np.float32(0), np.float32(1)))
     if output_scale != "sigmoid":
         pred = lambda x: bool(np.array([x], np.float32) > cut_off)  # noqa: E731
     elif rule == "train":

@@ -22,8 +22,9 @@ What differs, by design:
   * Data: `--data_dir synthetic[:N]` uses the seeded synthetic patches; any other
     directory is read through the reference's split files ({k}-fold_{,non_}tumorable_data.npy) and
     decoded once into uint8 caches (`data.decode_patch_list`); normalisation and flips run on the
-    GPU. Only input_type 'RGB' and model_arch 'UNet_B' with the BCE loss are implemented (the CE
-    `UNet` variant is outside this path).
+    GPU. input_type 'RGB'; model_arch 'UNet_B' with loss 'BCElogit', or the CE `UNet`
+    (model_arch 'UNet', loss 'CE', n_cls 2: CrossEntropyLoss aux + calc_selective_risk_image, argmax
+    masks as train.py:207-219).
   * TensorBoard scalars are written when torch.utils.tensorboard is importable, otherwise as JSON
     lines in `{log_dir}/{train,valid}/scalars.jsonl`.
 """
@@ -168,9 +169,12 @@ def train(args, ckpt_dir, log_dir):
     from . import net_utils, parallel
     from .metrics import SegMetrics, pixel_accuracy
 
-    if args.model_arch != 'UNet_B' or args.loss != 'BCElogit':
-        raise NotImplementedError("the MI355X path implements model_arch 'UNet_B' with loss 'BCElogit' "
-                                  "(train.py:71-86); the CE `UNet` variant is out of scope")
+    ce = args.model_arch == 'UNet'
+    if (ce and args.loss != 'CE') or (not ce and args.loss != 'BCElogit'):
+        raise NotImplementedError("the MI355X path pairs model_arch 'UNet_B' with loss 'BCElogit' and 'UNet' "
+                                  "with 'CE' (train.py:71-86 allows the mixed pairs; they are not implemented)")
+    if ce and args.n_cls != 2:
+        raise NotImplementedError("the CE UNet's on-device metrics are binary: n_cls 2 (train.py:23 default)")
     if args.input_type != 'RGB':
         raise NotImplementedError("input_type 'RGB' only (GH / H_RGB need cv2 / skimage colour transforms)")
 
@@ -185,9 +189,14 @@ def train(args, ckpt_dir, log_dir):
 
     torch.manual_seed(args.seed)
     dt = torch.bfloat16 if args.compute_dtype == 'bf16' else torch.float32
-    net = S.UNet_B(args.input_type, selective=args.selective, compute_dtype=dt)
-    loss_A = S.BCEWithLogitsLoss()
-    loss_S = S.calc_selective_risk_image_b if args.selective else None
+    if ce:
+        net = S.UNet(args.input_type, args.n_cls, selective=args.selective, compute_dtype=dt)
+        loss_A = S.CrossEntropyLoss()
+        loss_S = S.calc_selective_risk_image if args.selective else None
+    else:
+        net = S.UNet_B(args.input_type, selective=args.selective, compute_dtype=dt)
+        loss_A = S.BCEWithLogitsLoss()
+        loss_S = S.calc_selective_risk_image_b if args.selective else None
 
     start_epoch = 0
     if os.path.exists(ckpt_dir) and os.listdir(ckpt_dir):  # train.py:113-127 (network weights only)
@@ -220,30 +229,35 @@ def train(args, ckpt_dir, log_dir):
 
     writer_train = _Scalars(os.path.join(log_dir, 'train'), rank == 0)
     writer_val = _Scalars(os.path.join(log_dir, 'valid'), rank == 0)
-    ev_train = SegMetrics(device, selective=bool(args.selective), rule="train", output_scale=args.output_scale)
-    ev_val = SegMetrics(device, selective=bool(args.selective), rule="train", output_scale=args.output_scale)
+    rule = "argmax" if ce else "train"
+    ev_train = SegMetrics(device, selective=bool(args.selective), rule=rule, output_scale=args.output_scale)
+    ev_val = SegMetrics(device, selective=bool(args.selective), rule=rule, output_scale=args.output_scale)
+
+    def binary(t):  # CE logits (N, 2, H, W) -> the fp32 difference the argmax rule thresholds at 0
+        return (t[:, 1] - t[:, 0]).contiguous() if ce else t
     history = []
 
     def run_epoch(loader, training, ev):
         sums = torch.zeros(3, dtype=torch.float64, device=device)  # loss, aux loss, selection loss
         steps = 0
         for x, target in loader:
+            tgt = target.long() if ce else target  # train.py:189-191 (int64 labels for CE)
             if args.selective:
                 output, selection, aux = net(x)
-                aux_loss = loss_A(aux, target)
-                select_loss, coverage = loss_S(output, selection, target=target, lamb=args.s_lamb)
+                aux_loss = loss_A(aux, tgt)
+                select_loss, coverage = loss_S(output, selection, target=tgt, lamb=args.s_lamb)
                 loss = aux_loss + select_loss
                 sums[1] += aux_loss.detach()
                 sums[2] += select_loss.detach()
             else:
                 output, selection = net(x), None
-                loss = loss_A(output, target)
+                loss = loss_A(output, tgt)
             if training:
                 optim.zero_grad()
                 loss.backward()
                 optim.step()
             sums[0] += loss.detach()
-            ev.add_batch(output.detach(), target, None if selection is None else selection.detach())
+            ev.add_batch(binary(output.detach()), target, None if selection is None else binary(selection.detach()))
             steps += 1
         return sums, steps
 

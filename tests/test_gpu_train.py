@@ -181,3 +181,15 @@ def test_eval_cli_matches_oracle_metrics(tmp_path):
     got = np.array(res["confusion_matrix"])
     assert np.abs(got - cm).sum() <= 1e-3 * lab.size, (got, cm)
     assert abs(res["rejection_ratio"] - (1 - sel.mean())) <= 1e-3
+
+
+def test_train_cli_ce_unet(tmp_path):
+    """--model_arch UNet --loss CE (the reference's defaults, train.py:42,54): CE UNet, CrossEntropyLoss
+    aux + calc_selective_risk_image, argmax masks; checkpoint in the reference's UNet layout."""
+    out = _cli(tmp_path, "--model_arch", "UNet", "--loss", "CE", "--n_epoch", "1")
+    assert "train_loss" in out and "train_rejection" in out
+    sd = torch.load(tmp_path / "1-fold" / "checkpoint" / "model_epoch1.pth", map_location="cpu", weights_only=True)
+    assert list(sd["net"].keys()) == S.state_dict_keys("RGB", True, n_cls=2)
+    assert tuple(sd["net"]["conv_select.weight"].shape) == (2, 64, 1, 1)
+    hist = json.load(open(tmp_path / "1-fold" / "log" / "history.json"))
+    assert np.isfinite(hist[0]["train_loss"]) and 0 < sum(map(sum, hist[0]["train_cm"])) <= 3 * 8 * 64 * 64  # selected px

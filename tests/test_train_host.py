@@ -109,3 +109,13 @@ def test_construct_train_valid_matches_reference_split(tmp_path):
     assert np.array_equal(valid, np.vstack([out[0][1], out[1][1]]))
     test = D.construct_test(str(tmp_path), test_fold=2)
     assert len(test) == 9 + 13
+
+
+def test_argmax_rule_threshold_is_strict_positive():
+    """CE masks (train.py:207-219, np.argmax ties -> 0) are thresholded on x1 - x0 with `>= t`."""
+    import numpy as np
+    from selectivenet_for_semantic_segmentation_binary_amd.metrics import logit_threshold
+    t = np.float32(logit_threshold("argmax"))
+    assert t > 0 and np.nextafter(np.float32(0), np.float32(1)) == t
+    for d in (np.float32(0), np.float32(-0.0), np.float32(1e-45), np.float32(-1e-45), np.float32(3.0)):
+        assert bool(d >= t) == bool(d > 0)
