@@ -21,6 +21,12 @@
 
 #include "gemm_common.h"
 
+// SELUNET_GABL: timing ablations of gemm_gather (tools/ablate_gemm; results wrong unless 0):
+// 1 no epilogue store, 2 no MFMAs.
+#ifndef SELUNET_GABL
+#define SELUNET_GABL 0
+#endif
+
 namespace selunet {
 
 template <typename T, int BN, bool SMALL>
@@ -34,7 +40,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   constexpr int AR = BM / 32;                // A rows staged per thread
   constexpr int BR = BN / 32;                // B rows staged per thread
 
-  constexpr int SMEM_MAIN = 2 * (BM + BN) * ROWB, SMEM_EPI = BM * (BN + 4) * 4;
+  constexpr int SMEM_MAIN = 2 * (BM + BN) * ROWB, SMEM_EPI = BM * (BN + 4) * 4 + BM * 8;  // (+ row bases)
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
   unsigned char* As = smem;                          // [2][BM][ROWB]
   unsigned char* Bs = smem + 2 * BM * ROWB;          // [2][BN][ROWB]
@@ -191,10 +197,14 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 #pragma unroll
       for (int b = 0; b < NT; ++b)
         bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * WN + b * 32 + l32) * ROWB + boff);
+#if (SELUNET_GABL & 2)
+      asm volatile("" :: "v"(af[0].x ^ af[MT - 1].w), "v"(bfr[0].x ^ bfr[NT - 1].w));
+#else
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
+#endif
     }
   };
   for (int kc = 0; kc + 1 < nk; ++kc) {
@@ -212,22 +222,38 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
   __syncthreads();
   const int Cq = N >> 2;
+  // SCATTER2X: each tile row's output base (pixel (img, 2y, 2x) of the 2x-upsampled grid) decoded
+  // once into LDS past the tile, instead of three integer divisions per stored 16-B chunk
+  int64_t* rowbase = reinterpret_cast<int64_t*>(smem + BM * (BN + 4) * 4);
+  if (ep.mode == SELUNET_EP_SCATTER2X) {
+    if (tid < BM) {
+      const int64_t m = m0 + tid;
+      int64_t base = -1;
+      if (m < g.M) {
+        const unsigned mu = (unsigned)m, x = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
+        const unsigned y = t % (unsigned)g.h, img = t / (unsigned)g.h;
+        base = (((int64_t)img * (2 * g.h) + 2 * y) * (2 * g.w) + 2 * x) * Cq;
+      }
+      rowbase[tid] = base;
+    }
+    __syncthreads();
+  }
   auto dst = [&](int row, int c) -> T* {
+    const int col = n0 + c;
+    if (ep.mode == SELUNET_EP_SCATTER2X) {
+      const int64_t base = rowbase[row];
+      if (base < 0) return nullptr;
+      const int ab = col / Cq, cq = col - ab * Cq;
+      return reinterpret_cast<T*>(ep.out0) + base + ((int64_t)(ab >> 1) * (2 * g.w) + (ab & 1)) * Cq + cq;
+    }
     const int64_t m = m0 + row;
     if (m >= g.M) return nullptr;
-    const int col = n0 + c;
     if (ep.mode == SELUNET_EP_PLAIN) return reinterpret_cast<T*>(ep.out0) + m * N + col;
-    if (ep.mode == SELUNET_EP_SPLIT)
-      return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
-                            : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
-    const int ab = col / Cq, cq = col - ab * Cq;
-    const unsigned mu = (unsigned)m, x = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
-    const unsigned y = t % (unsigned)g.h, img = t / (unsigned)g.h;
-    return reinterpret_cast<T*>(ep.out0) +
-           (((int64_t)img * (2 * g.h) + 2 * y + (ab >> 1)) * (2 * g.w) + 2 * x + (ab & 1)) * Cq + cq;
+    return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                          : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
   };
   auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
-  lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, m_tile, n0, N));
+  if (!(SELUNET_GABL & 1)) lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, m_tile, n0, N));
 }
 
 // =========================================================================== gemm_wgrad
