@@ -2,6 +2,7 @@
 // reductions, BatchNorm finalize/backward, MaxPool2d(2), the 1x1 heads, the selective / BCE
 // losses and multi-tensor Adam. All NHWC loads are 4-channel vectors (16 B fp32 / 8 B bf16).
 #include <cstdarg>
+#include <cstdlib>
 #include <cmath>
 
 #include "common.h"
@@ -258,7 +259,7 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int64_t 
 // dy = k0*dA - k1 - k2*xhat = k0*dA - (k1 - k2*mean*invstd) - (k2*invstd)*y. Each thread owns a fixed
 // group of 8 channels (coefficients in registers) and strides over pixels: 16-B bf16 / 32-B fp32
 // vectors, one pass over dz and y, one write of dy.
-template <typename T>
+template <typename T, int U = 4>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -278,7 +279,6 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
     b[e] = coef[C + c + e] - k2i * mean[c + e];
   }
   // U pixels per thread and iteration, all loads issued before any use (loads in flight per wave)
-  constexpr int U = 4;
   const int64_t stride = (int64_t)gridDim.x * PL;
   auto one = [&](const f32x4& y0, const f32x4& y1, const f32x4& g0, const f32x4& g1, int64_t off) {
     f32x4 o0, o1;
@@ -465,6 +465,7 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
 
 // =========================================================================== 1x1 heads (C = 64)
 // 16 lanes per pixel, 4 channels per lane; 4 pixels per wave instruction.
+constexpr int HU = 4;
 template <typename T>
 __global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ w,
@@ -476,8 +477,7 @@ __global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float
   f32x4 wv[3];
   for (int h = 0; h < 3; ++h) wv[h] = h < nh ? *reinterpret_cast<const f32x4*>(w + h * 64 + c) : f32x4{0, 0, 0, 0};
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 4);
-  for (int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4); p < m; p += stride) {
-    f32x4 z = Vec4<T>::load(y + p * 64 + c);
+  auto one = [&](f32x4 z, int64_t p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) z[e] = fmaxf(z[e] * sc[e] + sh[e], 0.0f);
     float acc[3];
@@ -495,7 +495,17 @@ __global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float
         o2[p] = acc[2] + b[2];
       }
     }
+  };
+  // HU pixels per lane group and iteration, loads issued before any use
+  int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4);
+  for (; p + (HU - 1) * stride < m; p += HU * stride) {
+    f32x4 z[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) z[u] = Vec4<T>::load(y + (p + u * stride) * 64 + c);
+#pragma unroll
+    for (int u = 0; u < HU; ++u) one(z[u], p + u * stride);
   }
+  for (; p < m; p += stride) one(Vec4<T>::load(y + p * 64 + c), p);
 }
 
 template <typename T>
@@ -521,12 +531,10 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
   const int64_t rows = gridDim.x;
   const int64_t chunk = (m + rows - 1) / rows;
   const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(m, p0 + chunk);
-  for (int64_t p = p0 + (threadIdx.x >> 4); p < p1; p += (TPB >> 4)) {
-    const f32x4 yv = Vec4<T>::load(y + p * 64 + c);
+  auto one = [&](const f32x4& yv, const float* g, int64_t p) {
     f32x4 z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) z[e] = fmaxf(yv[e] * sc[e] + sh[e], 0.0f);
-    float g[3] = {g0[p], nh > 1 ? g1[p] : 0.0f, nh > 1 ? g2[p] : 0.0f};
     f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];
     Vec4<T>::store(dz + p * 64 + c, d);
     if (bn_slab) {
@@ -539,6 +547,26 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
       dw[h] += z * g[h];
       db[h] += g[h];
     }
+  };
+  int64_t p = p0 + (threadIdx.x >> 4);
+  constexpr int PS = TPB >> 4;
+  for (; p + (HU - 1) * PS < p1; p += HU * PS) {
+    f32x4 yv[HU];
+    float g[HU][3];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int64_t q = p + u * PS;
+      yv[u] = Vec4<T>::load(y + q * 64 + c);
+      g[u][0] = g0[q];
+      g[u][1] = nh > 1 ? g1[q] : 0.0f;
+      g[u][2] = nh > 1 ? g2[q] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) one(yv[u], g[u], p + u * PS);
+  }
+  for (; p < p1; p += PS) {
+    const float g[3] = {g0[p], nh > 1 ? g1[p] : 0.0f, nh > 1 ? g2[p] : 0.0f};
+    one(Vec4<T>::load(y + p * 64 + c), g, p);
   }
   // block reduce: 16 pixel lanes per channel group
   __shared__ float red[TPB][13];
@@ -1039,7 +1067,14 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
   SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
                   "bn_bwd_apply: bad arguments");
   SELUNET_REQUIRE(ok_channels(c), "bn_bwd_apply: C must be 64, 128, 256 or 512 (got %d)", c);
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), 4096));
+  static const int u8 = [] { const char* v = getenv("SELUNET_APPLY_U"); return v && v[0] == '8'; }();
+  static const int64_t gcap = [] { const char* v = getenv("SELUNET_APPLY_GRID"); return v ? atoll(v) : 1024LL; }();
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), gcap));
+  if (u8) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(blocks), dim3(TPB), 0, as_stream(stream),
+                                         (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd, coef, (T*)dy));
+    return check_launch("bn_bwd_apply");
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(TPB), 0,
                                        as_stream(stream), (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd,
                                        coef, (T*)dy));
