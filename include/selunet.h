@@ -133,6 +133,11 @@ int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t
  * per MI355X CU; wgs <= 0 restores the default). Returns the previous value. The stats-slab row
  * count depends on it: query selunet_gemm_stats_rows after changing it. Not thread-safe. */
 int32_t selunet_set_halo_workgroups(int32_t wgs);
+/* Tuning/testing knob: workgroups the persistent generic gather GEMM (ConvTranspose2d forward and
+ * data gradient, 3x3 layers the halo kernels do not take) targets: default 512 (two per CU), 0 = one
+ * output tile per workgroup, < 0 restores the default. Returns the previous value. Changes the
+ * stats-slab row count like selunet_set_halo_workgroups. Not thread-safe. */
+int32_t selunet_set_gather_workgroups(int32_t wgs);
 /* Name of the kernel a selunet_gemm_gather (q == NULL; mode = epilogue mode) or
  * selunet_gemm_wgrad (q = the Q operand) call with these operands dispatches to. */
 const char* selunet_gemm_kernel_name(const selunet_gather* a, const selunet_gather* q, int32_t n_cols,

@@ -70,6 +70,7 @@ SIGNATURES = {
     "selunet_gemm_wgrad_ws": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, P, c_int64, c_int32, P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
+    "selunet_set_gather_workgroups": (c_int32, [c_int32]),
     "selunet_gemm_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), c_int32, c_int32,
                                                    c_int32]),
     "selunet_reduce_ws_bytes": (c_int64, [c_int32]),

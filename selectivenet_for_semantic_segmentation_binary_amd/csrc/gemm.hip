@@ -26,12 +26,23 @@
 #ifndef SELUNET_GABL
 #define SELUNET_GABL 0
 #endif
+// SELUNET_GPF: K stages of the gather GEMM in flight in registers (1 or 2)
+#ifndef SELUNET_GPF
+#define SELUNET_GPF 1
+#endif
 
 namespace selunet {
 
+// Persistent over output tiles: workgroup (prow, n_tile) owns column block n_tile and the row tiles
+// prow, prow + P, prow + 2P, ...; its K stages run as one continuous pipeline across tile
+// boundaries, so the first stage of the next tile is loading while this tile's last MFMAs and its
+// epilogue run (short-K GEMMs — ConvTranspose2d with K = 128..512 — are otherwise one exposed load
+// latency + one exposed epilogue per tile). Statistics accumulate in registers over the tiles and
+// are written once per workgroup (slab row prow). P = number of row tiles gives the one-tile-per-
+// workgroup launch.
 template <typename T, int BN, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
-gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles) {
+gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int P) {
   constexpr int E = 16 / sizeof(T);          // elements per 16-B vector
   constexpr int BKE = 128 / sizeof(T);       // K elements per stage
   constexpr int WN = BN / 2;                 // wave tile columns
@@ -53,26 +64,14 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 
   const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
   const int n_tile = lb % n_tiles;
-  const int64_t m_tile = lb / n_tiles;
-  const int64_t m0 = m_tile * BM;
+  const int64_t prow = lb / n_tiles;
   const int n0 = n_tile * BN;
+  const int64_t m_tiles = (g.M + BM - 1) / BM;
+  const int nk = k_pad / BKE;
+  const int64_t total = (m_tiles - prow + P - 1) / P * nk;  // stages of this workgroup (prow < P <= m_tiles)
 
   const int cc = tid & 7;       // 16-B chunk within the 128-B K slice
   const int rr = tid >> 3;      // base row (0..31)
-
-  // per-thread row coordinates of the A rows it stages
-  int ry[AR], rx[AR], rimg[AR];
-  bool rv[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int64_t m = m0 + rr + 32 * i;
-    rv[i] = m < g.M;
-    const int64_t mm = rv[i] ? m : 0;
-    rx[i] = (int)(mm % g.w);
-    const int64_t t = mm / g.w;
-    ry[i] = (int)(t % g.h);
-    rimg[i] = (int)(t / g.h);
-  }
 
   // One staged K slice, held in registers between its loads and its LDS write. Loads are issued
   // unconditionally (rows / pixels clamped to valid addresses, zeroed when written to LDS) so the
@@ -86,9 +85,10 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     int src;
   };
 
-  auto load_stage = [&](int kc) __attribute__((always_inline)) {
+  auto load_stage = [&](int64_t m_tile, int kc) __attribute__((always_inline)) {
     Stage st;
     const int k0 = kc * BKE;
+    const int64_t m0 = m_tile * BM;
     st.ok = 0;
     st.src = 0;
     if constexpr (!SMALL) {
@@ -114,11 +114,16 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       }
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
+        const int64_t m = m0 + rr + 32 * i;
+        const bool rv = m < g.M;
+        const unsigned mu = rv ? (unsigned)m : 0u;  // M < 2^31 (host check)
+        const unsigned rx = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
+        const unsigned ry = t % (unsigned)g.h, rimg = t / (unsigned)g.h;
         int ys, xs;
-        if (rv[i] && src_pixel(g, tap, ry[i], rx[i], ys, xs)) st.ok |= 1u << i;
+        if (rv && src_pixel(g, tap, (int)ry, (int)rx, ys, xs)) st.ok |= 1u << i;
         ys = min(max(ys, 0), g.hs - 1);
         xs = min(max(xs, 0), g.ws - 1);
-        const int64_t off = (((int64_t)rimg[i] * g.hs + ys) * g.ws + xs) * sa.C + st_c;
+        const int64_t off = (((int64_t)rimg * g.hs + ys) * g.ws + xs) * sa.C + st_c;
         st.a[i] = *reinterpret_cast<const uint4*>(base + off);
       }
     } else {
@@ -171,20 +176,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       *reinterpret_cast<uint4*>(b_dst + (rr + 32 * i) * ROWB + cc * 16) = st.b[i];
   };
 
-  f32x16 acc[MT][NT];
-#pragma unroll
-  for (int a = 0; a < MT; ++a)
-#pragma unroll
-    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
-
-  const int nk = k_pad / BKE;
-  {
-    const Stage st0 = load_stage(0);
-    store_stage(st0, 0);
-  }
-  __syncthreads();
-
-  auto mma_stage = [&](int buf) __attribute__((always_inline)) {
+  auto mma_stage = [&](f32x16 (&acc)[MT][NT], int buf) __attribute__((always_inline)) {
     const unsigned char* a_src = As + buf * BM * ROWB;
     const unsigned char* b_src = Bs + buf * BN * ROWB;
 #pragma unroll
@@ -207,26 +199,19 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 #endif
     }
   };
-  for (int kc = 0; kc + 1 < nk; ++kc) {
-    const Stage nxt = load_stage(kc + 1);
-    __builtin_amdgcn_sched_barrier(0);  // all of the next stage's loads ahead of this stage's MFMAs
-    mma_stage(kc & 1);
-    store_stage(nxt, (kc & 1) ^ 1);
-    __syncthreads();
-  }
-  mma_stage((nk - 1) & 1);
-  __syncthreads();
 
   // ------------------------------------------------------------------ epilogue (LDS-staged)
-  float* tile = reinterpret_cast<float*>(smem);  // [BM][BN + 4]; the loop ended with a barrier
-  acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
-  __syncthreads();
-  const int Cq = N >> 2;
-  // SCATTER2X: each tile row's output base (pixel (img, 2y, 2x) of the 2x-upsampled grid) decoded
-  // once into LDS past the tile, instead of three integer divisions per stored 16-B chunk
+  float* tile = reinterpret_cast<float*>(smem);  // [BM][BN + 4] over the (idle) stage buffers
   int64_t* rowbase = reinterpret_cast<int64_t*>(smem + BM * (BN + 4) * 4);
-  if (ep.mode == SELUNET_EP_SCATTER2X) {
-    if (tid < BM) {
+  const int Cq = N >> 2;
+  const TileStats ts = tile_stats(ep, prow, n0, N);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto epilogue = [&](const f32x16 (&acc)[MT][NT], int64_t m_tile) __attribute__((always_inline)) {
+    const int64_t m0 = m_tile * BM;
+    acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
+    // SCATTER2X: each tile row's output base (pixel (img, 2y, 2x) of the 2x-upsampled grid) decoded
+    // once into LDS past the tile, instead of three integer divisions per stored 16-B chunk
+    if (ep.mode == SELUNET_EP_SCATTER2X && tid < BM) {
       const int64_t m = m0 + tid;
       int64_t base = -1;
       if (m < g.M) {
@@ -237,23 +222,107 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       rowbase[tid] = base;
     }
     __syncthreads();
-  }
-  auto dst = [&](int row, int c) -> T* {
-    const int col = n0 + c;
-    if (ep.mode == SELUNET_EP_SCATTER2X) {
-      const int64_t base = rowbase[row];
-      if (base < 0) return nullptr;
-      const int ab = col / Cq, cq = col - ab * Cq;
-      return reinterpret_cast<T*>(ep.out0) + base + ((int64_t)(ab >> 1) * (2 * g.w) + (ab & 1)) * Cq + cq;
-    }
-    const int64_t m = m0 + row;
-    if (m >= g.M) return nullptr;
-    if (ep.mode == SELUNET_EP_PLAIN) return reinterpret_cast<T*>(ep.out0) + m * N + col;
-    return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
-                          : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+    auto dst = [&](int row, int c) -> T* {
+      const int col = n0 + c;
+      if (ep.mode == SELUNET_EP_SCATTER2X) {
+        const int64_t base = rowbase[row];
+        if (base < 0) return nullptr;
+        const int ab = col / Cq, cq = col - ab * Cq;
+        return reinterpret_cast<T*>(ep.out0) + base + ((int64_t)(ab >> 1) * (2 * g.w) + (ab & 1)) * Cq + cq;
+      }
+      const int64_t m = m0 + row;
+      if (m >= g.M) return nullptr;
+      if (ep.mode == SELUNET_EP_PLAIN) return reinterpret_cast<T*>(ep.out0) + m * N + col;
+      return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                            : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+    };
+    auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
+    if (!(SELUNET_GABL & 1))
+      lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
   };
-  auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
-  if (!(SELUNET_GABL & 1)) lds_tile_store<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, m_tile, n0, N));
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  {
+    const Stage st0 = load_stage(prow, 0);
+    store_stage(st0, 0);
+  }
+  __syncthreads();
+
+  int64_t mt = prow;
+  int kc = 0;
+#if SELUNET_GPF == 2
+  // two stages in flight: stage s+2 loads while s multiplies and s+1 (loaded one iteration ago)
+  // waits in registers for its LDS write
+  auto adv = [&](int64_t& m, int& k) {
+    if (k + 1 == nk) {
+      k = 0;
+      m += P;
+    } else {
+      ++k;
+    }
+  };
+  int64_t mt1 = mt;
+  int kc1 = kc;
+  adv(mt1, kc1);
+  Stage n1 = load_stage(total > 1 ? mt1 : mt, total > 1 ? kc1 : kc);
+  for (int64_t s = 0; s < total; ++s) {
+    const bool last_k = kc + 1 == nk;
+    int64_t mt2 = mt1;
+    int kc2 = kc1;
+    adv(mt2, kc2);
+    const bool has2 = s + 2 < total;
+    const Stage n2 = load_stage(has2 ? mt2 : mt, has2 ? kc2 : kc);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_stage(acc, (int)(s & 1));
+    if (last_k) {
+      __syncthreads();
+      epilogue(acc, mt);
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+      __syncthreads();
+    }
+    if (s + 1 < total) store_stage(n1, (int)((s + 1) & 1));
+    __syncthreads();
+    n1 = n2;
+    mt = mt1;
+    kc = kc1;
+    mt1 = mt2;
+    kc1 = kc2;
+  }
+#else
+  for (int64_t s = 0; s < total; ++s) {
+    const bool last_k = kc + 1 == nk;
+    const bool more = s + 1 < total;
+    const int64_t nmt = last_k ? mt + P : mt;
+    const int nkc = last_k ? 0 : kc + 1;
+    // the next stage (of this tile or the next one) loads while this one multiplies; the last
+    // stage reloads its own slice (valid addresses, never stored)
+    const Stage nxt = load_stage(more ? nmt : mt, more ? nkc : kc);
+    __builtin_amdgcn_sched_barrier(0);  // all of the next stage's loads ahead of this stage's MFMAs
+    mma_stage(acc, (int)(s & 1));
+    if (last_k) {
+      __syncthreads();  // both stage buffers idle: the tile is staged over them
+      epilogue(acc, mt);
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+      __syncthreads();
+    }
+    if (more) store_stage(nxt, (int)((s + 1) & 1));
+    __syncthreads();
+    mt = nmt;
+    kc = nkc;
+  }
+#endif
+  tile_stats_flush<BN, 256>(tile, tid, ts, s1, s2, s3);
 }
 
 // =========================================================================== gemm_wgrad
@@ -668,12 +737,34 @@ static void launch_gather(const GatherArg& g, const void* b, int N, int k_pad, c
   launch_gather_impl<T, BN, false>(g, b, N, k_pad, ep, st);
 }
 
+// Resident gather-GEMM workgroups the persistent launch aims for (2 per CU; a constant, not the
+// device's CU count, so slab rows never depend on the device); 0 = one tile per workgroup.
+// SELUNET_GATHER_WGS (profiling) or selunet_set_gather_workgroups (tests) override it.
+static int64_t gather_wgs_default() {
+  static const int64_t v = [] {
+    const char* e = getenv("SELUNET_GATHER_WGS");
+    return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)512;
+  }();
+  return v;
+}
+int64_t GATHER_WGS = -1;  // < 0: default
+static int64_t gather_wgs() { return GATHER_WGS < 0 ? gather_wgs_default() : GATHER_WGS; }
+
+// Row-tile workgroups (= statistics slab rows) of the gather GEMM for N output columns; independent
+// of the column tile width (64 or 128) so the caller can size slabs from (operand, N) alone.
+static int64_t gather_rows(const GatherArg& g, int N) {
+  const int64_t m_tiles = cdiv(g.M, BM);
+  const int64_t wgs = gather_wgs();
+  if (wgs == 0) return m_tiles;
+  return std::max<int64_t>(1, std::min<int64_t>(m_tiles, wgs / cdiv(N, 128)));
+}
+
 template <typename T, int BN, bool SMALL>
 static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
   const int n_tiles = N / BN;
-  const int64_t m_tiles = cdiv(g.M, BM);
-  hipLaunchKernelGGL((gemm_gather_kernel<T, BN, SMALL>), dim3((unsigned)(m_tiles * n_tiles)), dim3(256), 0, st, g,
-                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles);
+  const int64_t P = gather_rows(g, N);
+  hipLaunchKernelGGL((gemm_gather_kernel<T, BN, SMALL>), dim3((unsigned)(P * n_tiles)), dim3(256), 0, st, g,
+                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, (int)P);
 }
 
 template <typename T, int BI, int BJ>
@@ -710,12 +801,18 @@ bool selunet::halo_enabled() {
   return on;
 }
 
+extern "C" int32_t selunet_set_gather_workgroups(int32_t wgs) {
+  const int32_t prev = (int32_t)selunet::gather_wgs();
+  selunet::GATHER_WGS = wgs < 0 ? -1 : wgs;
+  return prev;
+}
+
 extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_cols, int32_t dtype) {
   const int esz = dtype == SELUNET_F32 ? 4 : 2;
   GatherArg g;
   if (make_gather(a, dtype, g, 16 / esz)) return -1;
   if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_stats_rows(g, n_cols, dtype);
-  return cdiv(g.M, BM);
+  return gather_rows(g, n_cols);
 }
 
 // Name of the kernel selunet_gemm_gather / selunet_gemm_wgrad dispatch to for these operands

@@ -43,6 +43,20 @@ def halo_wgs():
         K.query("selunet_set_halo_workgroups", prev[0])
 
 
+@pytest.fixture
+def gather_wgs():
+    """Set the persistent gather GEMM's workgroup target for one test (-1 = default, 0 = one tile per
+    workgroup), restored after."""
+    prev = []
+
+    def set_(wgs):
+        prev.append(K.query("selunet_set_gather_workgroups", wgs))
+
+    yield set_
+    if prev:
+        K.query("selunet_set_gather_workgroups", prev[0])
+
+
 def gen(*shape, seed=0, scale=1.0):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(*shape, generator=g) * scale
@@ -132,9 +146,12 @@ def test_conv3x3_fwd_small_c_nchw():
                                                 (64, 128, 0, 8, 8), (64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
                                                 (256, 128, 128, 16, 48), (64, 32, 0, 24, 20), (128, 32, 64, 16, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
-def test_conv3x3_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+def test_conv3x3_dgrad(cin, cout, split, h, w, wgs, halo_wgs, gather_wgs):
+    """wgs = 3 also sets the generic gather GEMM (the 8x8 cases, 3 row tiles at n = 6) to one workgroup
+    row: one workgroup walks every tile and accumulates the column / BN-backward sums over them."""
     halo_wgs(wgs)
-    n = 2
+    gather_wgs(wgs - 2 if wgs else -1)
+    n = 6 if h == 8 else 2
     wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
     dy = gen(n, cout, h, w, seed=7)
     x = gen(n, cin, h, w, seed=8).requires_grad_()
@@ -207,8 +224,12 @@ def test_conv3x3_wgrad(cin0, cin1, cout, xform, small):
 
 
 @pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64)])
-def test_convT_fwd_bwd(cin, cout):
-    n, h, w = 2, 4, 6
+@pytest.mark.parametrize("gwgs", [-1, 0, 3, 16])
+def test_convT_fwd_bwd(cin, cout, gwgs, gather_wgs):
+    """4 row tiles (the last one ragged): one tile per workgroup (0), every tile in one workgroup
+    (3), two tiles per workgroup (16 at 1024 columns) and the default persistent launch."""
+    gather_wgs(gwgs)
+    n, h, w = 2, 13, 18
     x = gen(n, cin, h, w, seed=13)
     s, t = bn_fold(cin, 30)
     a = torch.relu(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1)).requires_grad_()

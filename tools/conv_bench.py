@@ -1,6 +1,6 @@
 """Per-layer timing of the 3x3 conv kernels at the bench shapes (bs=128, bf16) — profiling tool.
 
-    python tools/conv_bench.py [--batch 128] [--iters 20] [--only fwd|dgrad] [--layers enc1_2,dec1_2]
+    python tools/conv_bench.py [--batch 128] [--iters 20] [--only fwd|dgrad|wgrad] [--layers enc1_2,dec1_2]
 
 Calls selunet_gemm_gather directly on random NHWC operands (forward: BN+ReLU transform of the
 producer applied on load, BN-stat epilogue; dgrad: untransformed dY, the SPLIT epilogue where the
@@ -73,6 +73,47 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16):
     return ms, flops / (ms * 1e-3) / 1e12, name, (keep, o0, o1, stats, w)
 
 
+def run_wgrad(n, c_srcs, co, hw, iters, dt=torch.bfloat16):
+    """Weight gradient P^T Q: P = dY [m][co] (1 tap), Q = the layer input gather (9 taps, BN+ReLU of
+    the producers), deterministic split partials + reduction (the training default)."""
+    dev = "cuda"
+    keep, srcs = [], []
+    for c in c_srcs:
+        if c == 0:
+            continue
+        x = torch.randn(n, hw, hw, c, device=dev).to(dt)
+        sc, sh = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1
+        keep += [x, sc, sh]
+        srcs.append(K.source(x, c, sc, sh, relu=True))
+    ci = sum(c_srcs)
+    dy = torch.randn(n, hw, hw, co, device=dev).to(dt)
+    gp = K.gather(n, hw, hw, 1, K.source(dy, co))
+    gq = K.gather(n, hw, hw, 9, *srcs)
+    ld = K.query("selunet_wgrad_ld", 9 * ci)
+    out = torch.empty(co, ld, device=dev)
+    code = K.dtype_code(dt)
+    wsb = K.query("selunet_gemm_wgrad_ws_bytes", ctypes.byref(gp), ctypes.byref(gq), code)
+    ws = torch.empty(max(wsb // 4, 1), device=dev)
+    name = K.query("selunet_gemm_kernel_name", ctypes.byref(gp), ctypes.byref(gq), co, 0, code).decode()
+
+    def call():
+        K.call("selunet_gemm_wgrad_ws", ctypes.byref(gp), ctypes.byref(gq), K.ptr(out), K.ptr(ws), wsb, code,
+               K.stream_ptr())
+
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        call()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    flops = 2.0 * n * hw * hw * co * 9 * ci
+    return ms, flops / (ms * 1e-3) / 1e12, name
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
@@ -85,11 +126,17 @@ def main():
     for name, (c0, c1), co, hw in LAYERS:
         if sel and name not in sel:
             continue
-        if a.only != "dgrad":
+        if a.only not in ("dgrad", "wgrad"):
             ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
+        if a.only == "wgrad":
+            ms, tf, kn = run_wgrad(a.batch, (c0, c1), co, hw, a.iters)
+            tot_ms += ms
+            tot_fl += tf * ms
+            print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
+            continue
         if a.only != "fwd":
             ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters)
             tot_ms += ms
