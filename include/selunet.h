@@ -155,10 +155,37 @@ int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather* q, float* 
 int64_t selunet_gemm_wgrad_ws_bytes(const selunet_gather* p, const selunet_gather* q, int32_t dtype);
 int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gather* q, float* out, float* ws,
                           int64_t ws_bytes, int32_t dtype, void* stream);
+/* selunet_gemm_wgrad_ws with the result written in the reference parameter layout by the split
+ * reduction itself: layout 1 = Conv2d weight [co][ci][3][3] (P = dY, Q = the 3x3 input taps),
+ * layout 2 = ConvTranspose2d weight [ci][co][2][2] (P = the input, Q = the 4 output taps) — the
+ * .grad of model.py:11 / model.py:44,51,57 weights. `packed` ([ni][selunet_wgrad_ld] fp32) is
+ * scratch used only by operands without a split-partials path (may be NULL otherwise). */
+int selunet_gemm_wgrad_ws_to(const selunet_gather* p, const selunet_gather* q, float* packed,
+                             float* ws, int64_t ws_bytes, int32_t layout, float* out, int32_t dtype,
+                             void* stream);
 /* Row stride of the packed wgrad output for a Q operand with kq columns (kq rounded up to
  * the column tile); `out` must be [ni][selunet_wgrad_ld(kq)], the pad columns are garbage-free
  * zeros when out was zeroed. */
 int32_t selunet_wgrad_ld(int32_t kq);
+
+/* Every weight pack of a step in one launch: conv3x3 entries as selunet_pack_conv3x3 (fwd
+ * required, dgrad optional), ConvTranspose2d entries as selunet_pack_convT (w [ci][co][2][2]).
+ * `offset` is computed by the call. Replaces the per-tensor loop over model.py's conv/unpool
+ * parameters (model.py:11,44,51,57) that casting fp32 masters to the compute operands needs. */
+#define SELUNET_PACK_MAX 24
+enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1 };
+typedef struct selunet_pack_desc {
+  const float* w;
+  void* fwd;
+  void* dgrad;
+  int32_t kind, co, ci, k_pad;
+  int64_t offset;
+} selunet_pack_desc;
+typedef struct selunet_pack_list {
+  int32_t n, _pad;
+  selunet_pack_desc d[SELUNET_PACK_MAX];
+} selunet_pack_list;
+int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* stream);
 
 /* ---- reductions ----------------------------------------------------------------------- */
 /* out[c] = sum_r slab[r][c] in fp64, deterministic order, written as fp64 (out) and/or fp32
@@ -189,6 +216,22 @@ int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, c
 int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const float* gamma,
                             const float* invstd, float* dgamma, float* dbeta, float* dbias,
                             float* coef, void* stream);
+/* Fused forms used by the training step: the column sums of the statistics slab the producer
+ * wrote ([rows][2][C] sum/sumsq for the forward, [rows][3][C] for the backward) reduced in fp64
+ * (fixed order) and finalized in one launch (two above SELUNET_RF_SINGLE rows, default 1024).
+ * Same results as selunet_reduce_rows + selunet_bn_finalize(training = 1) /
+ * selunet_bn_bwd_finalize up to the fp64 summation order. ws: >= selunet_reduce_ws_bytes(2*C or
+ * 3*C); sums (fp64 [2|3][C]) may be NULL. Replace BatchNorm2d's batch-statistics pass
+ * (model.py:12) and its backward (autograd of model.py:12). */
+int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,
+                              int32_t c, const float* conv_bias, const float* gamma, const float* beta,
+                              float* running_mean, float* running_var, int64_t* num_batches,
+                              float momentum, float eps, float* mean, float* invstd, float* scale,
+                              float* shift, void* stream);
+int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums,
+                                  int64_t count, int32_t c, const float* gamma, const float* invstd,
+                                  float* dgamma, float* dbeta, float* dbias, float* coef,
+                                  void* stream);
 /* dy = coef0*dA - coef1 - coef2*xhat (the conv-output gradient). */
 int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
                          const float* shift, const float* mean, const float* invstd,

@@ -43,6 +43,19 @@ class Epilogue(ctypes.Structure):
                 ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats)]
 
 
+class PackDesc(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("fwd", c_void_p), ("dgrad", c_void_p), ("kind", c_int32), ("co", c_int32),
+                ("ci", c_int32), ("k_pad", c_int32), ("offset", c_int64)]
+
+
+PACK_MAX, PACK_CONV3X3, PACK_CONVT = 24, 0, 1
+WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
+
+
+class PackList(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("_pad", c_int32), ("d", PackDesc * PACK_MAX)]
+
+
 class HeadPlanes(ctypes.Structure):
     _fields_ = [("n", c_int32), ("hw", c_int32), ("plane", c_void_p * 8), ("img_stride", c_int64 * 8),
                 ("w_off", c_int32 * 8), ("b_off", c_int32 * 8), ("row_len", c_int32)]
@@ -68,6 +81,8 @@ SIGNATURES = {
     "selunet_wgrad_ld": (c_int32, [c_int32]),
     "selunet_gemm_wgrad_ws_bytes": (c_int64, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), c_int32]),
     "selunet_gemm_wgrad_ws": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, P, c_int64, c_int32, P]),
+    "selunet_gemm_wgrad_ws_to": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, P, c_int64, c_int32, P,
+                                           c_int32, P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
     "selunet_set_gather_workgroups": (c_int32, [c_int32]),
@@ -81,6 +96,10 @@ SIGNATURES = {
                                       P]),
     "selunet_bn_bwd_reduce": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_finalize": (c_int32, [P, c_int64, c_int32, P, P, P, P, P, P, P]),
+    "selunet_pack_weights": (c_int32, [ctypes.POINTER(PackList), c_int32, P]),
+    "selunet_bn_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, c_float, c_float,
+                                            P, P, P, P, P]),
+    "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),
     "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),

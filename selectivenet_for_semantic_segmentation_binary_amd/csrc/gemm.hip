@@ -888,7 +888,12 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
 }
 
 // Deterministic split reduction of the weight-gradient partials: out[i][j] = sum_s ws[s][i][j]
-// for j < kq (fixed split order), 0 in the pad columns.
+// for j < kq (fixed split order), 0 in the pad columns. LAYOUT != PACKED writes the reference
+// parameter layout instead of the packed [ni][ldo] one (the unpack pass folded into the reduction):
+// CONV3X3: packed column j = tap*ci + c of row o -> out[o][c][tap] (Conv2d weight [co][ci][3][3]);
+// CONVT: packed column j = ab*co + o of row c -> out[c][o][ab] (ConvTranspose2d weight [ci][co][2][2]).
+enum { WG_PACKED = 0, WG_CONV3X3 = 1, WG_CONVT = 2 };
+template <int LAYOUT>
 __global__ void __launch_bounds__(64) wgrad_reduce_kernel(const float* __restrict__ ws, int64_t splits,
                                                           int64_t stride, int ni, int ldo, int kq,
                                                           float* __restrict__ out) {
@@ -914,7 +919,23 @@ __global__ void __launch_bounds__(64) wgrad_reduce_kernel(const float* __restric
         for (int u = 0; u < 4; ++u)
           if (j + u >= kq) acc[u] = 0.0f;
     }
-    *reinterpret_cast<f32x4*>(out + e) = acc;
+    if constexpr (LAYOUT == WG_PACKED) {
+      *reinterpret_cast<f32x4*>(out + e) = acc;
+    } else {
+      const int64_t row = e / ldo;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = j + u;
+        if (jj >= kq) continue;
+        if constexpr (LAYOUT == WG_CONV3X3) {
+          const int ci = kq / 9, tap = jj / ci, c = jj - tap * ci;
+          out[(row * ci + c) * 9 + tap] = acc[u];
+        } else {
+          const int co = kq / 4, ab = jj / co, o = jj - ab * co;
+          out[(row * co + o) * 4 + ab] = acc[u];
+        }
+      }
+    }
   }
 }
 
@@ -1003,9 +1024,41 @@ extern "C" int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gath
   launch_wgrad_any(w, out, ws, dtype, st);
   const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64), 0, st, ws, w.splits, (int64_t)w.ni * w.nj_pad,
+  hipLaunchKernelGGL(wgrad_reduce_kernel<WG_PACKED>, dim3(blocks), dim3(64), 0, st, ws, w.splits, (int64_t)w.ni * w.nj_pad,
                      w.ni, w.nj_pad, w.gq.K, out);
   return check_launch("gemm_wgrad_ws");
+}
+
+// selunet_gemm_wgrad_ws with the result written straight in the reference parameter layout
+// (layout 1: Conv2d [co][ci][3][3], 2: ConvTranspose2d [ci][co][2][2]); `packed` ([ni][ld] fp32)
+// is scratch for the operands without a split-partials path (atomics, then the unpack kernel).
+extern "C" int selunet_gemm_wgrad_ws_to(const selunet_gather* p, const selunet_gather* q, float* packed, float* ws,
+                                        int64_t ws_bytes, int32_t layout, float* out, int32_t dtype, void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad(p, q, dtype, w)) return rc;
+  SELUNET_REQUIRE(out != nullptr && (layout == WG_CONV3X3 || layout == WG_CONVT), "wgrad_ws_to: bad arguments");
+  SELUNET_REQUIRE(w.gq.K % (layout == WG_CONV3X3 ? 9 : 4) == 0, "wgrad_ws_to: K_q = %d is not a multiple of %d",
+                  w.gq.K, layout == WG_CONV3X3 ? 9 : 4);
+  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  if (need == 0) {
+    SELUNET_REQUIRE(packed != nullptr, "wgrad_ws_to: packed scratch is NULL");
+    if (int rc = selunet_gemm_wgrad_ws(p, q, packed, ws, ws_bytes, dtype, stream)) return rc;
+    return layout == WG_CONV3X3 ? selunet_unpack_conv3x3_grad(packed, w.ni, w.gq.K / 9, w.nj_pad, out, stream)
+                                : selunet_unpack_convT_grad(packed, w.ni, w.gq.K / 4, out, stream);
+  }
+  SELUNET_REQUIRE(ws != nullptr && ws_bytes >= need, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                  (long long)ws_bytes);
+  hipStream_t st = as_stream(stream);
+  launch_wgrad_any(w, nullptr, ws, dtype, st);
+  const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
+  if (layout == WG_CONV3X3)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
+                       (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONVT>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
+                       (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
+  return check_launch("gemm_wgrad_ws_to");
 }
 
 // leading dimension of the packed wgrad output for a Q operand with kq columns

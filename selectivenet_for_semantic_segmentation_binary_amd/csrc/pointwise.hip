@@ -94,6 +94,49 @@ __global__ void unpack_convT_kernel(const float* __restrict__ packed, int ci, in
   }
 }
 
+// All weight packs of a step in one launch (selunet_pack_weights): the list travels by value in
+// the kernel arguments; block b serves the tensor whose element range [off, off + total) holds
+// its first element, grid-striding over the concatenated element space.
+template <typename T>
+__global__ void pack_weights_kernel(selunet_pack_list l, int64_t total) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int t = 0;
+    while (t + 1 < l.n && i >= l.d[t + 1].offset) ++t;
+    const selunet_pack_desc& d = l.d[t];
+    const int64_t j = i - d.offset;
+    const float* w = d.w;
+    T* fwd = reinterpret_cast<T*>(d.fwd);
+    T* dg = reinterpret_cast<T*>(d.dgrad);
+    if (d.kind == SELUNET_PACK_CONV3X3) {  // as pack_conv3x3_kernel
+      const int co = d.co, ci = d.ci, k_pad = d.k_pad;
+      const int64_t total_f = (int64_t)co * k_pad;
+      if (j < total_f) {
+        const int o = (int)(j / k_pad), k = (int)(j % k_pad);
+        float v = 0.0f;
+        if (k < 9 * ci) {
+          const int tap = k / ci, c = k - tap * ci;
+          v = w[((int64_t)o * ci + c) * 9 + tap];
+        }
+        fwd[j] = from_f<T>(v);
+      } else {
+        const int64_t q = j - total_f;
+        const int c = (int)(q / (9 * co));
+        const int k = (int)(q % (9 * co));
+        const int tap = k / co, o = k - tap * co;
+        dg[q] = from_f<T>(w[((int64_t)o * ci + c) * 9 + (8 - tap)]);
+      }
+    } else {  // as pack_convT_kernel: w[c][o][ab]
+      const int ci = d.ci, co = d.co;
+      const int ab = (int)(j & 3);
+      const int64_t co_ci = j >> 2;
+      const int o = (int)(co_ci % co), c = (int)(co_ci / co);
+      const T v = from_f<T>(w[j]);
+      if (fwd) fwd[((int64_t)ab * co + o) * ci + c] = v;
+      if (dg) dg[(int64_t)c * 4 * co + ab * co + o] = v;
+    }
+  }
+}
+
 static unsigned grid_for(int64_t n, int64_t cap = 4096) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, TPB), cap));
 }
@@ -186,31 +229,48 @@ __global__ void channel_sum_kernel(const T* __restrict__ x, int64_t m, int C, fl
 }
 
 // =========================================================================== BatchNorm
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t count, int C, const float* conv_bias,
-                                   const float* gamma, const float* beta, float* rmean, float* rvar,
-                                   int64_t* nbt, float momentum, float eps, int training, float* mean_o,
-                                   float* invstd_o, float* scale_o, float* shift_o) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (training && nbt && c == 0) *nbt += 1;
-  if (c >= C) return;
-  const double b = conv_bias ? (double)conv_bias[c] : 0.0;
+// one channel of the BatchNorm finalize: batch statistics from the fp64 sums (training) or the
+// running statistics (eval) -> mean (of the conv output without bias), invstd, folded scale/shift
+struct BnFinArgs {
+  int64_t count;
+  const float* conv_bias;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float momentum, eps;
+  int training;
+  float *mean_o, *invstd_o, *scale_o, *shift_o;
+};
+
+__device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const BnFinArgs& a) {
+  const double b = a.conv_bias ? (double)a.conv_bias[c] : 0.0;
   double mean, var;
-  if (training) {
-    mean = sums[c] / (double)count;
-    var = sums[C + c] / (double)count - mean * mean;
+  if (a.training) {
+    mean = s_sum / (double)a.count;
+    var = s_sq / (double)a.count - mean * mean;
     if (var < 0) var = 0;
-    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * (mean + b));
-    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * (double)count / (double)(count - 1));
+    if (a.rmean) a.rmean[c] = (float)((1.0 - a.momentum) * a.rmean[c] + a.momentum * (mean + b));
+    if (a.rvar)
+      a.rvar[c] = (float)((1.0 - a.momentum) * a.rvar[c] + a.momentum * var * (double)a.count / (double)(a.count - 1));
   } else {
-    mean = (double)rmean[c] - b;  // running stats track conv output *with* bias
-    var = (double)rvar[c];
+    mean = (double)a.rmean[c] - b;  // running stats track conv output *with* bias
+    var = (double)a.rvar[c];
   }
-  const double inv = 1.0 / sqrt(var + (double)eps);
-  const double sc = (double)gamma[c] * inv;
-  mean_o[c] = (float)mean;
-  invstd_o[c] = (float)inv;
-  scale_o[c] = (float)sc;
-  shift_o[c] = (float)((double)beta[c] - mean * sc);
+  const double inv = 1.0 / sqrt(var + (double)a.eps);
+  const double sc = (double)a.gamma[c] * inv;
+  a.mean_o[c] = (float)mean;
+  a.invstd_o[c] = (float)inv;
+  a.scale_o[c] = (float)sc;
+  a.shift_o[c] = (float)((double)a.beta[c] - mean * sc);
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, BnFinArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.training && a.nbt && c == 0) *a.nbt += 1;
+  if (c >= C) return;
+  bn_finalize_one(c, a.training ? sums[c] : 0.0, a.training ? sums[C + c] : 0.0, a);
 }
 
 template <typename T>
@@ -239,21 +299,111 @@ __global__ void bn_bwd_reduce_kernel(const T* __restrict__ dz, const T* __restri
   channel_block_reduce<3>(acc, C, slab + (int64_t)blockIdx.x * 3 * C);
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int64_t count, int C, const float* gamma,
-                                       const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef) {
+struct BnbFinArgs {
+  int64_t count;
+  const float* gamma;
+  const float* invstd;
+  float *dgamma, *dbeta, *dbias, *coef;
+};
+
+__device__ inline void bn_bwd_finalize_one(int c, int C, double sda, double sdax, double sx, const BnbFinArgs& a) {
+  const double k0 = (double)a.gamma[c] * a.invstd[c];
+  const double k1 = k0 * sda / (double)a.count;
+  const double k2 = k0 * sdax / (double)a.count;
+  if (a.dgamma) a.dgamma[c] = (float)sdax;
+  if (a.dbeta) a.dbeta[c] = (float)sda;
+  // sum over pixels of the conv-output gradient; analytically zero (BN removes the mean)
+  if (a.dbias) a.dbias[c] = (float)(k0 * sda - (double)a.count * k1 - k2 * sx);
+  a.coef[c] = (float)k0;
+  a.coef[C + c] = (float)k1;
+  a.coef[2 * C + c] = (float)k2;
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int C, BnbFinArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double sda = sums[c], sdax = sums[C + c], sx = sums[2 * C + c];
-  const double k0 = (double)gamma[c] * invstd[c];
-  const double k1 = k0 * sda / (double)count;
-  const double k2 = k0 * sdax / (double)count;
-  if (dgamma) dgamma[c] = (float)sdax;
-  if (dbeta) dbeta[c] = (float)sda;
-  // sum over pixels of the conv-output gradient; analytically zero (BN removes the mean)
-  if (dbias) dbias[c] = (float)(k0 * sda - (double)count * k1 - k2 * sx);
-  coef[c] = (float)k0;
-  coef[C + c] = (float)k1;
-  coef[2 * C + c] = (float)k2;
+  bn_bwd_finalize_one(c, C, sums[c], sums[C + c], sums[2 * C + c], a);
+}
+
+// Column sums of a [rows][SETS][C] slab (fp32 partials, or the fp64 first-level split sums) in
+// fp64, followed in the same launch by the per-channel BatchNorm finalize (forward, SETS = 2) or
+// BatchNorm-backward finalize (SETS = 3): one launch where reduce_rows + *_finalize took three.
+// 1024 threads = 16 row lanes x 64 channels; every lane keeps 8 rows x SETS loads in flight, the
+// 16 lane sums are added in a fixed order (deterministic).
+constexpr int RF_LANES = 16, RF_U = 8;
+template <typename S, int SETS>
+__global__ void __launch_bounds__(1024) reduce_finalize_kernel(const S* __restrict__ src, int64_t rows, int C,
+                                                               double* __restrict__ sums_out, BnFinArgs fa,
+                                                               BnbFinArgs ba) {
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int64_t cols = (int64_t)SETS * C;
+  double acc[SETS];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) acc[s] = 0.0;
+  if (c < C) {
+    int64_t r = lane;
+    for (; r + (RF_U - 1) * RF_LANES < rows; r += RF_U * RF_LANES) {
+      S v[RF_U][SETS];
+#pragma unroll
+      for (int u = 0; u < RF_U; ++u)
+#pragma unroll
+        for (int s = 0; s < SETS; ++s) v[u][s] = src[(r + u * RF_LANES) * cols + s * C + c];
+#pragma unroll
+      for (int u = 0; u < RF_U; ++u)
+#pragma unroll
+        for (int s = 0; s < SETS; ++s) acc[s] += (double)v[u][s];
+    }
+    for (; r < rows; r += RF_LANES)
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) acc[s] += (double)src[r * cols + s * C + c];
+  }
+  __shared__ double red[SETS][RF_LANES][64];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) red[s][lane][cl] = acc[s];
+  __syncthreads();
+  if (SETS == 2 && fa.nbt && threadIdx.x == 0 && blockIdx.x == 0) *fa.nbt += 1;
+  if (lane != 0 || c >= C) return;
+  double t[SETS];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    double x = 0.0;
+#pragma unroll
+    for (int l = 0; l < RF_LANES; ++l) x += red[s][l][cl];
+    t[s] = x;
+    if (sums_out) sums_out[s * C + c] = x;
+  }
+  if constexpr (SETS == 2) bn_finalize_one(c, t[0], t[1], fa);
+  else bn_bwd_finalize_one(c, C, t[0], t[1], t[2], ba);
+}
+
+// rows up to which the fused reductions read the fp32 slab in one launch; above it a first level
+// (reduce_rows_l1) cuts the rows to <= RED_SPLITS fp64 split sums first (SELUNET_RF_SINGLE)
+static int64_t rf_single_rows() {
+  static const int64_t v = [] {
+    const char* e = getenv("SELUNET_RF_SINGLE");
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+  }();
+  return v;
+}
+
+// slab [rows][SETS][c] fp32 -> launches of the fused reduce + finalize (ws: >= selunet_reduce_ws_bytes(SETS*c))
+template <int SETS>
+static void launch_reduce_finalize(const float* slab, int64_t rows, int c, double* ws, double* sums,
+                                   const BnFinArgs& fa, const BnbFinArgs& ba, hipStream_t st) {
+  const unsigned blocks = (unsigned)cdiv(c, 64);
+  if (rows <= rf_single_rows()) {
+    hipLaunchKernelGGL((reduce_finalize_kernel<float, SETS>), dim3(blocks), dim3(1024), 0, st, slab, rows, c, sums,
+                       fa, ba);
+    return;
+  }
+  const int cols = SETS * c;
+  const int splits = (int)std::min<int64_t>(RED_SPLITS, cdiv(rows, 16));
+  const int64_t chunk = cdiv(rows, splits);
+  hipLaunchKernelGGL(reduce_rows_l1, dim3((unsigned)cdiv(cols, 64), splits), dim3(TPB), 0, st, slab, rows, cols, chunk,
+                     ws);
+  hipLaunchKernelGGL((reduce_finalize_kernel<double, SETS>), dim3(blocks), dim3(1024), 0, st, ws, (int64_t)splits, c,
+                     sums, fa, ba);
 }
 
 // dy = k0*dA - k1 - k2*xhat = k0*dA - (k1 - k2*mean*invstd) - (k2*invstd)*y. Each thread owns a fixed
@@ -974,6 +1124,27 @@ int selunet_pack_convT(const float* w, int32_t ci, int32_t co, void* fwd, void* 
   return check_launch("pack_convT");
 }
 
+int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(list && list->n > 0 && list->n <= SELUNET_PACK_MAX, "pack_weights: bad list");
+  selunet_pack_list l = *list;
+  int64_t off = 0;
+  for (int t = 0; t < l.n; ++t) {
+    selunet_pack_desc& d = l.d[t];
+    SELUNET_REQUIRE(d.w && (d.fwd || d.dgrad) && d.co > 0 && d.ci > 0, "pack_weights: bad entry %d", t);
+    d.offset = off;
+    if (d.kind == SELUNET_PACK_CONV3X3) {
+      SELUNET_REQUIRE(d.fwd && d.k_pad >= 9 * d.ci, "pack_weights: bad conv3x3 entry %d", t);
+      off += (int64_t)d.co * d.k_pad + (d.dgrad ? (int64_t)d.ci * 9 * d.co : 0);
+    } else {
+      SELUNET_REQUIRE(d.kind == SELUNET_PACK_CONVT, "pack_weights: bad kind in entry %d", t);
+      off += (int64_t)d.ci * d.co * 4;
+    }
+  }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weights_kernel<T>, dim3(grid_for(off, 8192)), dim3(TPB), 0,
+                                       as_stream(stream), l, off));
+  return check_launch("pack_weights");
+}
+
 int selunet_unpack_conv3x3_grad(const float* packed, int32_t co, int32_t ci, int32_t ld, float* out, void* stream) {
   SELUNET_REQUIRE(packed && out && co > 0 && ci > 0 && ld >= 9 * ci, "unpack_conv3x3_grad: bad arguments");
   hipLaunchKernelGGL(unpack_conv3x3_kernel, dim3(grid_for((int64_t)co * ci * 9)), dim3(TPB), 0, as_stream(stream),
@@ -1037,10 +1208,33 @@ int selunet_bn_finalize(const double* sums, int64_t count, int32_t c, const floa
   } else {
     SELUNET_REQUIRE(running_mean && running_var, "bn_finalize(eval): running stats are NULL");
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums, count,
-                     c, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, mean,
-                     invstd, scale, shift);
+  const BnFinArgs a{count, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
+                    mean, invstd, scale, shift};
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums, c, a);
   return check_launch("bn_finalize");
+}
+
+int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums, int64_t count, int32_t c,
+                              const float* conv_bias, const float* gamma, const float* beta, float* running_mean,
+                              float* running_var, int64_t* num_batches, float momentum, float eps, float* mean,
+                              float* invstd, float* scale, float* shift, void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && gamma && beta && mean && invstd && scale && shift && c > 0,
+                  "bn_stats_finalize: bad arguments");
+  SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
+  const BnFinArgs fa{count, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, 1,
+                     mean, invstd, scale, shift};
+  launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
+  return check_launch("bn_stats_finalize");
+}
+
+int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,
+                                  int32_t c, const float* gamma, const float* invstd, float* dgamma, float* dbeta,
+                                  float* dbias, float* coef, void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && gamma && invstd && coef && c > 0 && count > 0,
+                  "bn_bwd_stats_finalize: bad arguments");
+  const BnbFinArgs ba{count, gamma, invstd, dgamma, dbeta, dbias, coef};
+  launch_reduce_finalize<3>(slab, rows, c, ws, sums, BnFinArgs{}, ba, as_stream(stream));
+  return check_launch("bn_bwd_stats_finalize");
 }
 
 int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, const float* scale, const float* shift,
@@ -1056,8 +1250,8 @@ int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, c
 int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const float* gamma, const float* invstd,
                             float* dgamma, float* dbeta, float* dbias, float* coef, void* stream) {
   SELUNET_REQUIRE(sums && gamma && invstd && coef && c > 0 && count > 0, "bn_bwd_finalize: bad arguments");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums,
-                     count, c, gamma, invstd, dgamma, dbeta, dbias, coef);
+  const BnbFinArgs a{count, gamma, invstd, dgamma, dbeta, dbias, coef};
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(c, TPB)), dim3(TPB), 0, as_stream(stream), sums, c, a);
   return check_launch("bn_bwd_finalize");
 }
 

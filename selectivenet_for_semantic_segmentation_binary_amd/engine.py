@@ -135,10 +135,33 @@ class Engine:
         ws = K.keep(torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=packed.device)) if wsb > 0 else None
         K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, self.code, self.stream)
 
+    def _wgrad_param(self, gp, gq, layout, ni, ld, out):
+        """Weight gradient straight into the parameter's gradient in the reference layout
+        (layout WG_CONV3X3: [co][ci][3][3], WG_CONVT: [ci][co][2][2]); deterministic bf16 path: the
+        split reduction writes that layout itself (no packed copy, no unpack launch)."""
+        dev = out.device
+        if self.deterministic:
+            wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, self.code)
+            if wsb < 0:
+                raise RuntimeError(f"selunet_gemm_wgrad_ws_bytes: {K.load().selunet_last_error().decode()}")
+            if wsb > 0:
+                ws = K.keep(torch.empty(wsb // 4, dtype=torch.float32, device=dev))
+                K.call("selunet_gemm_wgrad_ws_to", gp, gq, None, K.ptr(ws), wsb, layout, K.ptr(out), self.code,
+                       self.stream)
+                return
+        packed = K.keep(torch.empty(ni, ld, dtype=torch.float32, device=dev))
+        self._wgrad(gp, gq, packed)
+        if layout == K.WG_CONV3X3:
+            K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), ni, out.shape[1], ld, K.ptr(out),
+                   self.stream)
+        else:
+            K.call("selunet_unpack_convT_grad", K.ptr(packed), ni, out.shape[1], K.ptr(out), self.stream)
+
     def pack_weights(self, P, need_dgrad=True):
-        """fp32 master weights -> GEMM operand layouts in the compute dtype."""
+        """fp32 master weights -> GEMM operand layouts in the compute dtype (one launch for all)."""
         dev = P["encoder_layer_1_2.0.weight"].device
         packs = {}
+        pl = K.PackList()
         for name, ci, co in LY.CBR_LAYERS:
             w = P[f"{name}.0.weight"]
             ci = w.shape[1]
@@ -147,14 +170,17 @@ class Engine:
             dg = None
             if need_dgrad and name != "encoder_layer_1_1":
                 dg = K.keep(torch.empty(ci, 9 * co, dtype=self.dt, device=dev))
-            K.call("selunet_pack_conv3x3", K.ptr(w), co, ci, kpad, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
+            pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONV3X3, co, ci, kpad, 0)
+            pl.n += 1
             packs[name] = (fwd, dg, kpad)
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
             fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
             dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
-            K.call("selunet_pack_convT", K.ptr(w), ci, co, K.ptr(fwd), K.ptr(dg), self.code, self.stream)
+            pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
+            pl.n += 1
             packs[name] = (fwd, dg, ci)
+        K.call("selunet_pack_weights", pl, self.code, self.stream)
         return packs
 
     # ------------------------------------------------------------------ forward pieces
@@ -181,14 +207,18 @@ class Engine:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
             K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
         mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
-        sums = None
-        if ctx.training:
-            sums = K.keep(torch.empty(2 * co, dtype=torch.float64, device=dev))
-            self._reduce(stats, rows, 2 * co, out64=sums)
-        K.call("selunet_bn_finalize", K.ptr(sums), M, co, K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]),
-               K.ptr(P[f"{name}.1.bias"]), K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
-               K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, int(ctx.training),
-               K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+        if ctx.training:  # statistics slab -> fp64 column sums -> batch mean/invstd, running stats: one launch
+            ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
+            K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
+                   K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+                   K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
+                   K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS,
+                   K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+        else:
+            K.call("selunet_bn_finalize", None, M, co, K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]),
+                   K.ptr(P[f"{name}.1.bias"]), K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
+                   K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, 0,
+                   K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
         st = BNState(y, mean, invstd, scale, shift, n, h, w, co)
         ctx.bn[name] = st
         return st
@@ -363,13 +393,12 @@ class Engine:
         pair for a concatenated input (d(up) with its column sums)."""
         st: BNState = ctx.bn[name]
         M, co, dev = st.n * st.h * st.w, st.c, st.y.device
-        sums = K.keep(torch.empty(3 * co, dtype=torch.float64, device=dev))
-        self._reduce(dg.slab, dg.rows, 3 * co, out64=sums)
         coef = K.keep(torch.empty(3, co, dtype=torch.float32, device=dev))
         gamma = ctx.params[f"{name}.1.weight"]
-        K.call("selunet_bn_bwd_finalize", K.ptr(sums), M, co, K.ptr(gamma), K.ptr(st.invstd),
-               K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]), K.ptr(coef),
-               self.stream)
+        ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 3 * co) // 8, dtype=torch.float64, device=dev))
+        K.call("selunet_bn_bwd_stats_finalize", K.ptr(dg.slab), dg.rows, K.ptr(ws), None, M, co, K.ptr(gamma),
+               K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]),
+               K.ptr(coef), self.stream)
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
@@ -388,11 +417,9 @@ class Engine:
             return None
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
-        packed = K.keep(torch.empty(co, ld, dtype=torch.float32, device=dev))
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
-        self._wgrad(gp, gq, packed)
-        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, ci, ld, K.ptr(G[f"{name}.0.weight"]), self.stream)
+        self._wgrad_param(gp, gq, K.WG_CONV3X3, co, ld, G[f"{name}.0.weight"])
         K.marker(("grads", name))
         if not need_dgrad:
             return None
@@ -425,11 +452,9 @@ class Engine:
         dev = du.t.device
         self._reduce(du.slab, du.rows, co, out32=G[f"{name}.bias"])
         ld = K.query("selunet_wgrad_ld", 4 * co)
-        packed = K.keep(torch.empty(ci, ld, dtype=torch.float32, device=dev))
         gp = K.gather(n, h, w, 1, prev.src())
         gq = K.gather(n, h, w, 4, K.source(du.t, co))
-        self._wgrad(gp, gq, packed)
-        K.call("selunet_unpack_convT_grad", K.ptr(packed), ci, co, K.ptr(G[f"{name}.weight"]), self.stream)
+        self._wgrad_param(gp, gq, K.WG_CONVT, ci, ld, G[f"{name}.weight"])
         K.marker(("grads", name))
         dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))

@@ -376,6 +376,140 @@ def test_reduce_rows_deterministic():
     assert rel(outs[0], slab.double().sum(0).cpu()) < 1e-12
 
 
+# ---------------------------------------------------------------- fused launches (launch-count cuts)
+@pytest.mark.parametrize("rows", [1, 37, 1024, 1025, 5000])
+@pytest.mark.parametrize("c", [64, 192, 512])
+def test_bn_stats_finalize_matches_reduce_then_finalize(rows, c):
+    """selunet_bn_stats_finalize / selunet_bn_bwd_stats_finalize (one launch at <= 1024 rows, two
+    above) against selunet_reduce_rows + the separate finalize kernels: fp64 sums equal to 1e-12,
+    finalized outputs to fp32 rounding; bit-reproducible across calls."""
+    M = 4096
+    slab2 = (gen(rows, 2, c, seed=40) + torch.tensor([0.3, 1.2]).view(1, 2, 1)).to(DEV)
+    slab2[:, 1] = slab2[:, 1].abs() * 3  # sum of squares stays above mean^2 * count
+    slab3 = gen(rows, 3, c, seed=41).to(DEV)
+    bias, gamma, beta = gen(c, seed=42).to(DEV) * 0.1, gen(c, seed=43).abs().to(DEV) + 0.5, gen(c, seed=44).to(DEV)
+    ws = torch.empty(K.query("selunet_reduce_ws_bytes", 3 * c) // 8, dtype=torch.float64, device=DEV)
+
+    def fwd_fused():
+        rm, rv = torch.full((c,), 0.1, device=DEV), torch.ones(c, device=DEV)
+        nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+        o = [torch.empty(c, device=DEV) for _ in range(4)]
+        sums = torch.empty(2 * c, dtype=torch.float64, device=DEV)
+        K.call("selunet_bn_stats_finalize", K.ptr(slab2), rows, K.ptr(ws), K.ptr(sums), M, c, K.ptr(bias),
+               K.ptr(gamma), K.ptr(beta), K.ptr(rm), K.ptr(rv), K.ptr(nbt), 0.1, 1e-5, *[K.ptr(t) for t in o],
+               K.stream_ptr())
+        return sums, [rm, rv] + o, int(nbt)
+
+    def fwd_ref():
+        rm, rv = torch.full((c,), 0.1, device=DEV), torch.ones(c, device=DEV)
+        nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+        o = [torch.empty(c, device=DEV) for _ in range(4)]
+        sums = torch.empty(2 * c, dtype=torch.float64, device=DEV)
+        K.call("selunet_reduce_rows", K.ptr(slab2), rows, 2 * c, K.ptr(ws), K.ptr(sums), None, K.stream_ptr())
+        K.call("selunet_bn_finalize", K.ptr(sums), M, c, K.ptr(bias), K.ptr(gamma), K.ptr(beta), K.ptr(rm),
+               K.ptr(rv), K.ptr(nbt), 0.1, 1e-5, 1, *[K.ptr(t) for t in o], K.stream_ptr())
+        return sums, [rm, rv] + o, int(nbt)
+
+    s_f, o_f, n_f = fwd_fused()
+    s_f2, o_f2, _ = fwd_fused()
+    s_r, o_r, n_r = fwd_ref()
+    assert n_f == n_r == 1
+    assert rel(s_f, slab2.double().sum(0).reshape(-1)) < 1e-12
+    assert rel(s_f, s_r) < 1e-12
+    assert torch.equal(s_f, s_f2) and all(torch.equal(a, b) for a, b in zip(o_f, o_f2))
+    for a, b in zip(o_f, o_r):
+        assert rel(a, b) < 1e-6
+
+    def bwd(fused):
+        sums = torch.empty(3 * c, dtype=torch.float64, device=DEV)
+        invstd = o_r[3]
+        o = [torch.empty(c, device=DEV) for _ in range(3)] + [torch.empty(3, c, device=DEV)]
+        if fused:
+            K.call("selunet_bn_bwd_stats_finalize", K.ptr(slab3), rows, K.ptr(ws), K.ptr(sums), M, c, K.ptr(gamma),
+                   K.ptr(invstd), *[K.ptr(t) for t in o], K.stream_ptr())
+        else:
+            K.call("selunet_reduce_rows", K.ptr(slab3), rows, 3 * c, K.ptr(ws), K.ptr(sums), None, K.stream_ptr())
+            K.call("selunet_bn_bwd_finalize", K.ptr(sums), M, c, K.ptr(gamma), K.ptr(invstd), *[K.ptr(t) for t in o],
+                   K.stream_ptr())
+        return sums, o
+
+    s_f, o_f = bwd(True)
+    s_r, o_r2 = bwd(False)
+    assert rel(s_f, slab3.double().sum(0).reshape(-1)) < 1e-12 and rel(s_f, s_r) < 1e-12
+    for a, b in zip(o_f[:2] + o_f[3:], o_r2[:2] + o_r2[3:]):
+        assert rel(a, b) < 1e-6
+    # dbias is analytically zero: only rounding noise, bounded by the terms it cancels
+    assert float((o_f[2] - o_r2[2]).abs().max()) < 1e-6 * float(o_r2[0].abs().max() * M + 1)
+
+
+def test_pack_weights_matches_per_tensor_packs():
+    """One selunet_pack_weights launch over conv3x3 (with/without dgrad) and ConvTranspose2d
+    entries equals the per-tensor pack entry points bit for bit (bf16 and fp32)."""
+    specs = [("c", 64, 3, 32), ("c", 128, 64, 576), ("c", 256, 512, 4608), ("t", 256, 512, 0), ("c", 64, 128, 1152),
+             ("t", 64, 128, 0)]
+    for dt, code in ((torch.bfloat16, K.BF16), (torch.float32, K.F32)):
+        pl = K.PackList()
+        outs = []
+        for i, (kind, co, ci, kpad) in enumerate(specs):
+            if kind == "c":
+                w = gen(co, ci, 3, 3, seed=50 + i).to(DEV)
+                fwd = torch.empty(co, kpad, dtype=dt, device=DEV)
+                dg = torch.empty(ci, 9 * co, dtype=dt, device=DEV) if ci != 3 else None
+                ref_f, ref_d = torch.empty_like(fwd), (torch.empty_like(dg) if dg is not None else None)
+                K.call("selunet_pack_conv3x3", K.ptr(w), co, ci, kpad, K.ptr(ref_f), K.ptr(ref_d), code, K.stream_ptr())
+                pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONV3X3, co, ci, kpad, 0)
+            else:
+                w = gen(ci, co, 2, 2, seed=50 + i).to(DEV)
+                fwd = torch.empty(4 * co, ci, dtype=dt, device=DEV)
+                dg = torch.empty(ci, 4 * co, dtype=dt, device=DEV)
+                ref_f, ref_d = torch.empty_like(fwd), torch.empty_like(dg)
+                K.call("selunet_pack_convT", K.ptr(w), ci, co, K.ptr(ref_f), K.ptr(ref_d), code, K.stream_ptr())
+                pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
+            pl.n += 1
+            outs.append((w, fwd, dg, ref_f, ref_d))
+        K.call("selunet_pack_weights", pl, code, K.stream_ptr())
+        torch.cuda.synchronize()
+        for w, fwd, dg, ref_f, ref_d in outs:
+            assert torch.equal(fwd, ref_f)
+            if dg is not None:
+                assert torch.equal(dg, ref_d)
+
+
+@pytest.mark.parametrize("kind,n,h,w,cp,cq", [("c", 2, 16, 16, 64, 64), ("c", 2, 32, 32, 128, 64),
+                                              ("c", 1, 8, 8, 256, 512), ("t", 2, 16, 16, 128, 64),
+                                              ("t", 2, 8, 8, 512, 256)])
+def test_wgrad_ws_to_matches_packed_then_unpack(kind, n, h, w, cp, cq):
+    """selunet_gemm_wgrad_ws_to (split reduction writing the reference weight layout) equals
+    selunet_gemm_wgrad_ws + the unpack entry point bit for bit, for Conv2d 3x3 (halo and generic
+    wgrad paths) and ConvTranspose2d operands."""
+    M = n * h * w
+    p = gen(M, cp, seed=60).to(DEV).to(torch.bfloat16)
+    if kind == "c":
+        q = gen(M, cq, seed=61).to(DEV).to(torch.bfloat16)
+        gp, gq = K.gather(n, h, w, 1, K.source(p, cp)), K.gather(n, h, w, 9, K.source(q, cq))
+        kq, ni, layout = 9 * cq, cp, K.WG_CONV3X3
+        out_ref = torch.empty(cp, cq, 3, 3, device=DEV)
+    else:
+        q = gen(4 * M, cq, seed=61).to(DEV).to(torch.bfloat16)  # the 2x-upsampled output gradient
+        gp, gq = K.gather(n, h, w, 1, K.source(p, cp)), K.gather(n, h, w, 4, K.source(q, cq))
+        kq, ni, layout = 4 * cq, cp, K.WG_CONVT
+        out_ref = torch.empty(cp, cq, 2, 2, device=DEV)
+    ld = K.query("selunet_wgrad_ld", kq)
+    wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, K.BF16)
+    assert wsb > 0
+    ws = torch.empty(wsb // 4, device=DEV)
+    packed = torch.empty(ni, ld, device=DEV)
+    K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, K.BF16, K.stream_ptr())
+    if kind == "c":
+        K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cp, cq, ld, K.ptr(out_ref), K.stream_ptr())
+    else:
+        K.call("selunet_unpack_convT_grad", K.ptr(packed), cp, cq, K.ptr(out_ref), K.stream_ptr())
+    out = torch.full_like(out_ref, float("nan"))
+    K.call("selunet_gemm_wgrad_ws_to", gp, gq, None, K.ptr(ws), wsb, layout, K.ptr(out), K.BF16, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref)
+
+
 def _bf(t):
     return t.to(torch.bfloat16).float()
 
