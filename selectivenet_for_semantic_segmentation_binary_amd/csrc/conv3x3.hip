@@ -812,7 +812,15 @@ int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int64_
   const int bi = ni % 128 == 0 ? 128 : 64;
   const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
   const int64_t total = (int64_t)q.n * cdiv(q.w, WTW) * cdiv(q.h, WTH);
-  const int64_t want = std::max<int64_t>(1, cdiv(512, (int64_t)co_tiles * ci_chunks));
+  // workgroup target over (co tile, ci chunk, pixel split); each split adds ni*ld*4 bytes of
+  // partials for the fixed-order reduction to read. One workgroup per CU (256) measured best:
+  // 6.53 vs 6.94 ms/step at 16 images/GPU (512: two per CU, twice the partials), 11.8 vs 12.2 at
+  // 32, equal at 128; 128 and 384 lose (SELUNET_WGRAD_WGS overrides)
+  static const int64_t target = [] {
+    const char* e = getenv("SELUNET_WGRAD_WGS");
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
+  }();
+  const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
   const int64_t per = cdiv(total, std::min(total, want));
   if (per_out) *per_out = per;
   return cdiv(total, per);
