@@ -722,7 +722,14 @@ static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out
 
 // pixel splits of the generic weight gradient (rows per split a multiple of the 64-pixel stage)
 static int64_t wgrad_splits(int64_t M, int tiles, int64_t* mchunk_out) {
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(2048, tiles)));
+  // workgroup target over (tile, pixel split): 512 (two per CU) measured 6.43 vs 6.57 ms/step at
+  // 16 images/GPU against 2048 (fewer split partials to reduce), equal at 128; 256 and 1024 in
+  // between (SELUNET_GEMM_WGRAD_WGS overrides)
+  static const int64_t target = [] {
+    const char* e = getenv("SELUNET_GEMM_WGRAD_WGS");
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)512;
+  }();
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(target, tiles)));
   const int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
   if (mchunk_out) *mchunk_out = mchunk;
   return cdiv(M, mchunk);
