@@ -797,8 +797,198 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
   }
 }
 
+// fp32 weight gradient (v_mfma_f32_32x32x2_f32: exact fp32 products, the parity configuration).
+// Same wave roles as the bf16 kernel on an 8 x 8-pixel tile (10 x 10 halo: the register-held
+// prefetch of the next tile then fits beside the 9 tap accumulators without spilling); an MFMA operand is one fp32 per lane
+// (A[i = co][k = pixel], B[k = pixel][j = ci]), read with ds_read_b32 straight from the natural
+// [pixel][channel] tiles: lanes 0-31 take pixel 2s and lanes 32-63 pixel 2s + 1, the two 32-lane
+// groups of ds_read_b32 never conflict with each other and 32 consecutive floats in a group hit 32
+// distinct banks, so the tiles need no padding or swizzle. One dY fragment feeds the MFMAs of all
+// the wave's taps (9, or 5/4 when BI = 64). At the fp32 MFMA rate a pixel tile keeps every SIMD
+// busy for ~70k cycles, so one LDS buffer is enough: the next tile's loads are in registers during
+// the current tile's MFMAs and are written (BN+ReLU applied, padding zeroed) between two barriers.
+// (A 16-pixel-wide tile would need 56 prefetch registers per lane and spills at 2 waves per SIMD.)
+constexpr int FTH = 8, FTW = 8;                  // fp32 pixel tile
+
+template <int BI>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int co_tiles,
+                              int ci_chunks, int64_t tiles_per_split, int tiles_x, int tiles_y, int64_t total_tiles,
+                              float* __restrict__ ws, int64_t ws_stride) {
+  constexpr int CJ = 64;                         // ci channels per chunk
+  constexpr int WTH = FTH, WTW = FTW, WHW = FTW + 2, WPIXT = FTH * FTW, WHP = (FTH + 2) * (FTW + 2);
+  constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
+  constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
+  constexpr int P_ROUNDS = (WPIXT * BI / 4) / 512;
+  constexpr int X_ROUNDS = (WHP * (CJ / 4) + 511) / 512;
+  static_assert(P_ROUNDS * 512 == WPIXT * BI / 4, "dY tile must split evenly over the threads");
+
+  __shared__ __attribute__((aligned(16))) float Ps[WPIXT][BI];
+  __shared__ __attribute__((aligned(16))) float Xs[WHP][CJ];
+  __shared__ float Ks[2 * BI + 2 * CJ];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wj = wave & 1;
+  const int wi = (wave >> 1) % (BI / 32);
+  const int tg = (wave >> 1) / (BI / 32);
+  const int tap0 = tg * 5;
+  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int cot = lb % co_tiles;
+  const int rest = lb / co_tiles;
+  const int cik = rest % ci_chunks;
+  const int64_t split = rest / ci_chunks;
+  const int i0 = cot * BI;
+  const int c0 = cik * CJ;
+  const int64_t pt_begin = split * tiles_per_split;
+  const int64_t pt_end = min(total_tiles, pt_begin + tiles_per_split);
+  if (pt_begin >= pt_end) return;
+
+  int xs_src = 0, xc = c0;
+  if (Q.nsrc > 1 && xc >= Q.src[0].C) {
+    xc -= Q.src[0].C;
+    xs_src = 1;
+  }
+  const SrcArg xa = pick_src(Q, xs_src);
+  const SrcArg& pa = P.src[0];
+  const int H = P.h, W = P.w;
+
+  if (tid < 2 * BI + 2 * CJ) {
+    float v;
+    if (tid < 2 * BI) {
+      const int c = i0 + (tid % BI);
+      v = pa.scale ? (tid < BI ? pa.scale[c] : pa.shift[c]) : 0.0f;
+    } else {
+      const int c = xc + ((tid - 2 * BI) % CJ);
+      v = xa.scale ? (tid < 2 * BI + CJ ? xa.scale[c] : xa.shift[c]) : 0.0f;
+    }
+    Ks[tid] = v;
+  }
+
+  auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
+    x0 = ((unsigned)pt - r2 * (unsigned)tiles_x) * WTW;
+    const unsigned r3 = r2 / (unsigned)tiles_y;
+    y0 = (r2 - r3 * (unsigned)tiles_y) * WTH;
+    img = (int)r3;
+  };
+  auto apply = [&](f32x4 v, const float* sc, const float* sh, int relu) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float f = v[j] * sc[j] + sh[j];
+      v[j] = relu ? fmaxf(f, 0.0f) : f;
+    }
+    return v;
+  };
+  f32x4 rp[P_ROUNDS], rx[X_ROUNDS];
+  auto load_tile = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      const int y = min(y0 + px / WTW, H - 1), x = min(x0 + px % WTW, W - 1);
+      rp[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pa.data) +
+                                              (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4);
+    }
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int hp = min(idx >> 4, WHP - 1), cc = idx & 15;
+      const int y = min(max(y0 - 1 + hp / WHW, 0), H - 1), x = min(max(x0 - 1 + hp % WHW, 0), W - 1);
+      rx[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(xa.data) +
+                                              (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 4);
+    }
+  };
+  auto store_tile = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (y0 + px / WTW < H && x0 + px % WTW < W)
+        v = pa.scale ? apply(rp[r], Ks + cc * 4, Ks + BI + cc * 4, pa.relu) : rp[r];
+      *reinterpret_cast<f32x4*>(&Ps[px][cc * 4]) = v;
+    }
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      if (idx < WHP * (CJ / 4)) {
+        const int hp = idx >> 4, cc = idx & 15;
+        const int y = y0 - 1 + hp / WHW, x = x0 - 1 + hp % WHW;
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          v = xa.scale ? apply(rx[r], Ks + 2 * BI + cc * 4, Ks + 2 * BI + CJ + cc * 4, xa.relu) : rx[r];
+        *reinterpret_cast<f32x4*>(&Xs[hp][cc * 4]) = v;
+      }
+    }
+  };
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
+
+  // per-lane LDS element offsets: dY column, halo column and each tap's halo pixel offset
+  const float* pcol = &Ps[0][wi * 32 + l32];
+  const float* xcol = &Xs[0][wj * 32 + l32];
+  int toff[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) {
+    const int tap = min(tap0 + t, 8);
+    toff[t] = ((tap / 3) * WHW + tap % 3) * CJ;
+  }
+
+  load_tile((int)pt_begin);
+  __syncthreads();  // coefficients visible
+  store_tile((int)pt_begin);
+  __syncthreads();
+  for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+    const bool more = pt + 1 < (int)pt_end;
+    load_tile(more ? pt + 1 : pt);
+    __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
+#pragma unroll 1
+    for (int ks = 0; ks < WPIXT / 2; ++ks) {
+      const int p = 2 * ks + half;                        // k = pixel of this lane's half
+      const float a = pcol[p * BI];
+      const int hbase = ((p / WTW) * WHW + p % WTW) * CJ;  // halo pixel of tap (0, 0)
+      float b[NTAP];
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t) b[t] = xcol[hbase + toff[t]];
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t)
+        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[t], acc[t], 0, 0, 0);
+    }
+    __syncthreads();  // every wave is done reading the tile
+    if (more) {
+      store_tile(pt + 1);
+      __syncthreads();
+    }
+  }
+
+  const int ctot = Q.Ctot;
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) {
+    if (t < ntap) {
+      const int tap = tap0 + t;
+      const int j = tap * ctot + c0 + wj * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[t][r];
+        else atomicAdd(out + (int64_t)i * ldo + j, acc[t][r]);
+      }
+    }
+  }
+}
+
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype) {
-  if (dtype != SELUNET_BF16) return false;
+  if (dtype != SELUNET_BF16 && dtype != SELUNET_F32) return false;
   if (p.taps != 1 || p.nsrc != 1 || p.small || p.src[0].layout != 0 || p.K % 64 != 0) return false;
   if (q.taps != 9 || q.small || q.h < 8 || q.w < 16) return false;
   for (int s = 0; s < q.nsrc; ++s)
@@ -807,11 +997,18 @@ bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dty
 }
 
 // pixel-tile splits of the halo weight gradient: ~512 workgroups over (co tile, ci chunk, split)
-int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
+static void wgrad_tile(int dtype, int& th, int& tw) {
+  th = dtype == SELUNET_F32 ? FTH : WTH;
+  tw = dtype == SELUNET_F32 ? FTW : WTW;
+}
+
+int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int dtype, int64_t* per_out) {
   const int ni = p.K;
   const int bi = ni % 128 == 0 ? 128 : 64;
   const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
-  const int64_t total = (int64_t)q.n * cdiv(q.w, WTW) * cdiv(q.h, WTH);
+  int th, tw;
+  wgrad_tile(dtype, th, tw);
+  const int64_t total = (int64_t)q.n * cdiv(q.w, tw) * cdiv(q.h, th);
   // workgroup target over (co tile, ci chunk, pixel split); each split adds ni*ld*4 bytes of
   // partials for the fixed-order reduction to read. One workgroup per CU (256) measured best:
   // 6.53 vs 6.94 ms/step at 16 images/GPU (512: two per CU, twice the partials), 11.8 vs 12.2 at
@@ -828,17 +1025,27 @@ int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int64_
 
 // ws == nullptr: fp32 atomics into out (zeroed by the caller). Otherwise every split writes its
 // partial to ws[split][ni][ldo] (ws_stride = ni * ldo floats) and the caller reduces the splits.
-int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, hipStream_t st) {
+int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
+                              hipStream_t st) {
   const int ni = p.K;
   const int bi = ni % 128 == 0 ? 128 : 64;
   const int co_tiles = ni / bi, ci_chunks = q.Ctot / 64;
-  const int tiles_x = (int)cdiv(q.w, WTW), tiles_y = (int)cdiv(q.h, WTH);
+  int th, tw;
+  wgrad_tile(dtype, th, tw);
+  const int tiles_x = (int)cdiv(q.w, tw), tiles_y = (int)cdiv(q.h, th);
   const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
   int64_t per;
-  const int64_t splits = conv3x3_wgrad_halo_splits(p, q, &per);
+  const int64_t splits = conv3x3_wgrad_halo_splits(p, q, dtype, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
   const int64_t stride = (int64_t)ni * ldo;
-  if (bi == 128)
+  if (dtype == SELUNET_F32) {
+    if (bi == 128)
+      hipLaunchKernelGGL(conv3x3_wgrad_halo_f32_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
+                         ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
+    else
+      hipLaunchKernelGGL(conv3x3_wgrad_halo_f32_kernel<64>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
+                         ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
+  } else if (bi == 128)
     hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
                        ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
   else

@@ -354,7 +354,7 @@ __device__ __forceinline__ f32x4 gather_vec4(const GatherArg& g, int64_t m, int 
 template <typename T, int BI, int BJ, bool SMALL>
 __global__ void __launch_bounds__(256, 2)
 gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk,
-                  int tiles_j, int tiles) {
+                  int tiles_j, int tiles, float* __restrict__ ws, int64_t ws_stride) {
   constexpr int KM = 32;              // pixels per stage
   constexpr int WI = BI / 2, WJ = BJ / 2;
   constexpr int MT = WI / 32, NT = WJ / 32;
@@ -456,7 +456,8 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + wi * WI + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
+        if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[a][b][r];
+        else atomicAdd(out + (int64_t)i * ldo + j, acc[a][b][r]);
       }
     }
 }
@@ -790,7 +791,7 @@ static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out
   const int64_t splits = wgrad_splits(p.M, tiles, &mchunk);
   if constexpr (std::is_same<T, float>::value)
     hipLaunchKernelGGL((gemm_wgrad_kernel<T, BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q, out,
-                       ldo, mchunk, tiles_j, tiles);
+                       ldo, mchunk, tiles_j, tiles, ws, (int64_t)ni * ldo);
   else
     hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<BI, BJ, SMALL>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, p, q,
                        out, ldo, mchunk, tiles_j, tiles, ws, (int64_t)ni * ldo);
@@ -847,8 +848,10 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
   GatherArg gq;
   const int vec = bf ? 8 : 4;
   if (make_gather(a, dtype, g, vec) || make_gather(q, dtype, gq, vec)) return "invalid";
-  if (halo_enabled() && conv3x3_wgrad_halo_eligible(g, gq, dtype))
-    return g.K % 128 == 0 ? "conv3x3_wgrad_halo<128>" : "conv3x3_wgrad_halo<64>";
+  if (halo_enabled() && conv3x3_wgrad_halo_eligible(g, gq, dtype)) {
+    if (bf) return g.K % 128 == 0 ? "conv3x3_wgrad_halo<128>" : "conv3x3_wgrad_halo<64>";
+    return g.K % 128 == 0 ? "conv3x3_wgrad_halo_f32<128>" : "conv3x3_wgrad_halo_f32<64>";
+  }
   return bf ? "gemm_wgrad_bf16" : "gemm_wgrad<f32>";
 }
 
@@ -950,7 +953,7 @@ struct WgradPlan {
   GatherArg gp, gq;
   int ni, bj, nj_pad;
   bool halo;
-  int64_t splits;  // 0: no split-partials path (fp32 / atomics only)
+  int64_t splits;  // pixel splits whose partials the fixed-order reduction sums
 };
 
 static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t dtype, WgradPlan& w) {
@@ -965,14 +968,11 @@ static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t 
   w.bj = (w.gq.K % 128 == 0 || w.gq.K > 512) ? 128 : 64;
   w.nj_pad = (int)(cdiv(w.gq.K, w.bj) * w.bj);
   w.halo = halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, dtype);
-  w.splits = 0;
-  if (dtype == SELUNET_BF16) {
-    if (w.halo) {
-      w.splits = conv3x3_wgrad_halo_splits(w.gp, w.gq, nullptr);
-    } else {
-      const int bi = w.ni % 128 == 0 ? 128 : 64;
-      w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
-    }
+  if (w.halo) {
+    w.splits = conv3x3_wgrad_halo_splits(w.gp, w.gq, dtype, nullptr);
+  } else {
+    const int bi = w.ni % 128 == 0 ? 128 : 64;
+    w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
   }
   return 0;
 }
@@ -981,16 +981,16 @@ static void launch_wgrad_any(const WgradPlan& w, float* out, float* ws, int32_t 
   const GatherArg &gp = w.gp, &gq = w.gq;
   const int ni = w.ni, nj_pad = w.nj_pad, bj = w.bj;
   if (w.halo) {
-    conv3x3_wgrad_halo_launch(gp, gq, out, nj_pad, ws, st);
+    conv3x3_wgrad_halo_launch(gp, gq, out, nj_pad, ws, dtype, st);
     return;
   }
   const bool bi128 = ni % 128 == 0;
   // out is [ni][nj_pad] where nj_pad = roundup(Kq, 64 or 128): see selunet_wgrad_ld()
   if (dtype == SELUNET_F32) {
-    if (bi128 && bj == 128) launch_wgrad<float, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else if (bj == 128) launch_wgrad<float, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else if (bi128) launch_wgrad<float, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
-    else launch_wgrad<float, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st);
+    if (bi128 && bj == 128) launch_wgrad<float, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else if (bj == 128) launch_wgrad<float, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else if (bi128) launch_wgrad<float, 128, 64>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
+    else launch_wgrad<float, 64, 64>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
   } else {
     if (bi128 && bj == 128) launch_wgrad<__bf16, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
     else if (bj == 128) launch_wgrad<__bf16, 64, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);

@@ -376,8 +376,9 @@ bool conv3x3_halo_persistent(const GatherArg& g, int dtype);            // multi
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
-int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, hipStream_t st);
-int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
+int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
+                              hipStream_t st);
+int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int dtype, int64_t* per_out);
 bool halo_enabled();
 
 }  // namespace selunet

@@ -186,10 +186,17 @@ def test_conv3x3_dgrad(cin, cout, split, h, w, wgs, halo_wgs, gather_wgs):
     assert rel(got, ref) < TOL
 
 
-@pytest.mark.parametrize("cin0,cin1,cout,xform,small", [(64, 0, 64, True, False), (64, 64, 128, True, False),
-                                                        (128, 0, 256, False, False), (3, 0, 64, False, True)])
-def test_conv3x3_wgrad(cin0, cin1, cout, xform, small):
-    n, h, w = 2, 16, 16
+@pytest.mark.parametrize("cin0,cin1,cout,xform,small,h,w", [
+    (64, 0, 64, True, False, 16, 16), (64, 64, 128, True, False, 16, 16), (128, 0, 256, False, False, 16, 16),
+    (3, 0, 64, False, True, 16, 16),
+    (64, 0, 64, True, False, 20, 36),     # fp32 halo wgrad: ragged 8x8 tiles, tap groups (BI = 64)
+    (128, 64, 128, True, False, 12, 16),  # fp32 halo wgrad: BI = 128, two sources, ragged rows
+    (64, 0, 128, False, False, 8, 8),     # generic fp32 wgrad (width below the halo tile)
+])
+def test_conv3x3_wgrad(cin0, cin1, cout, xform, small, h, w):
+    """fp32 weight gradient through both entry points: selunet_gemm_wgrad (fp32 atomics) and the
+    deterministic split-partials path selunet_gemm_wgrad_ws (fixed-order reduction)."""
+    n = 2
     x0 = gen(n, cin0, h, w, seed=9)
     x1 = gen(n, cin1, h, w, seed=10) if cin1 else None
     s0, t0 = bn_fold(cin0, 20)
@@ -221,6 +228,11 @@ def test_conv3x3_wgrad(cin0, cin1, cout, xform, small):
     out = torch.empty(cout, cin, 3, 3, device=DEV)
     K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cout, cin, ld, K.ptr(out), K.stream_ptr())
     assert rel(out.cpu(), ref) < TOL
+    if not small:
+        gp, gq = K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs)
+        det = wgrad_ws(gp, gq, packed, dtype=K.F32)
+        K.call("selunet_unpack_conv3x3_grad", K.ptr(det), cout, cin, ld, K.ptr(out), K.stream_ptr())
+        assert rel(out.cpu(), ref) < TOL
 
 
 @pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64)])
@@ -261,6 +273,10 @@ def test_convT_fwd_bwd(cin, cout, gwgs, gather_wgs):
            K.gather(n, h, w, 4, K.source(dud, cout)), K.ptr(packed), K.F32, K.stream_ptr())
     gwd = torch.empty(cin, cout, 2, 2, device=DEV)
     K.call("selunet_unpack_convT_grad", K.ptr(packed), cin, cout, K.ptr(gwd), K.stream_ptr())
+    assert rel(gwd.cpu(), gw) < TOL
+    det = wgrad_ws(K.gather(n, h, w, 1, K.source(xd, cin, sd, td)), K.gather(n, h, w, 4, K.source(dud, cout)), packed,
+                   dtype=K.F32)  # split partials + fixed-order reduction
+    K.call("selunet_unpack_convT_grad", K.ptr(det), cin, cout, K.ptr(gwd), K.stream_ptr())
     assert rel(gwd.cpu(), gw) < TOL
     Mu = n * 4 * h * w
     rows = K.query("selunet_channel_slab_rows", Mu)
@@ -478,34 +494,36 @@ def test_pack_weights_matches_per_tensor_packs():
 @pytest.mark.parametrize("kind,n,h,w,cp,cq", [("c", 2, 16, 16, 64, 64), ("c", 2, 32, 32, 128, 64),
                                               ("c", 1, 8, 8, 256, 512), ("t", 2, 16, 16, 128, 64),
                                               ("t", 2, 8, 8, 512, 256)])
-def test_wgrad_ws_to_matches_packed_then_unpack(kind, n, h, w, cp, cq):
+@pytest.mark.parametrize("code", [K.BF16, K.F32])
+def test_wgrad_ws_to_matches_packed_then_unpack(kind, n, h, w, cp, cq, code):
     """selunet_gemm_wgrad_ws_to (split reduction writing the reference weight layout) equals
     selunet_gemm_wgrad_ws + the unpack entry point bit for bit, for Conv2d 3x3 (halo and generic
     wgrad paths) and ConvTranspose2d operands."""
     M = n * h * w
-    p = gen(M, cp, seed=60).to(DEV).to(torch.bfloat16)
+    dt = torch.bfloat16 if code == K.BF16 else torch.float32
+    p = gen(M, cp, seed=60).to(DEV).to(dt)
     if kind == "c":
-        q = gen(M, cq, seed=61).to(DEV).to(torch.bfloat16)
+        q = gen(M, cq, seed=61).to(DEV).to(dt)
         gp, gq = K.gather(n, h, w, 1, K.source(p, cp)), K.gather(n, h, w, 9, K.source(q, cq))
         kq, ni, layout = 9 * cq, cp, K.WG_CONV3X3
         out_ref = torch.empty(cp, cq, 3, 3, device=DEV)
     else:
-        q = gen(4 * M, cq, seed=61).to(DEV).to(torch.bfloat16)  # the 2x-upsampled output gradient
+        q = gen(4 * M, cq, seed=61).to(DEV).to(dt)  # the 2x-upsampled output gradient
         gp, gq = K.gather(n, h, w, 1, K.source(p, cp)), K.gather(n, h, w, 4, K.source(q, cq))
         kq, ni, layout = 4 * cq, cp, K.WG_CONVT
         out_ref = torch.empty(cp, cq, 2, 2, device=DEV)
     ld = K.query("selunet_wgrad_ld", kq)
-    wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, K.BF16)
+    wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, code)
     assert wsb > 0
     ws = torch.empty(wsb // 4, device=DEV)
     packed = torch.empty(ni, ld, device=DEV)
-    K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, K.BF16, K.stream_ptr())
+    K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, code, K.stream_ptr())
     if kind == "c":
         K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), cp, cq, ld, K.ptr(out_ref), K.stream_ptr())
     else:
         K.call("selunet_unpack_convT_grad", K.ptr(packed), cp, cq, K.ptr(out_ref), K.stream_ptr())
     out = torch.full_like(out_ref, float("nan"))
-    K.call("selunet_gemm_wgrad_ws_to", gp, gq, None, K.ptr(ws), wsb, layout, K.ptr(out), K.BF16, K.stream_ptr())
+    K.call("selunet_gemm_wgrad_ws_to", gp, gq, None, K.ptr(ws), wsb, layout, K.ptr(out), code, K.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(out, out_ref)
 
