@@ -7,17 +7,28 @@ One step = the reference's training iteration (train.py:186-209) on synthetic, H
 data: forward of UNet_B(selective=True), BCEWithLogits aux loss + calc_selective_risk_image_b
 (s_lamb=2), backward (with the RCCL gradient all-reduce when N > 1) and the Adam update. The
 global batch of 128 is split into contiguous per-rank chunks (DataParallel semantics), so
-`scaling` is "strong". Rank 0 prints one JSON line. The `roofline` object is for the dominant
-kernel (the largest total time among the MFMA GEMM entry points, timed with HIP events on
-the launch stream over the whole timed region); `cpu_baseline` times the CPU oracle
-(oracle/unet_b_cpu.py, the reference's op sequence in torch eager on the host cores) on a
-bounded sample.
+`scaling` is "strong". Rank 0 prints one JSON line.
+
+`value` is the fp32 configuration — the reference's arithmetic (model.py:9-15, train.py:194-209),
+computed with exact-fp32 MFMA products (v_mfma_f32_32x32x2_f32) — timed with no profiling hook
+installed. The same run then measures the bf16 speed configuration (`bf16` key) the same way.
+For each configuration, after the headline timing:
+  * `roofline`: a separate pass with every kernel entry point bracketed by HIP events on the
+    launch stream; the dominant kernel's algorithmic FLOPs (MFMA-bound) or bytes (HBM-bound) per
+    launch divided by its average launch duration, against the MI355X peak for its bound;
+  * `full_loop`: the step plus the on-device train-loop metrics (train.py:211-241 restated:
+    thresholded masks, confusion matrix, rejection counts, loss sums; metrics.SegMetrics), read
+    back once at the end — SURVEY.md §8(d) timing (b).
+`cpu_baseline` times the CPU oracle (oracle/unet_b_cpu.py, the reference's op sequence in torch
+eager on the host cores) on a bounded sample.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
+import platform
 import sys
 import time
 
@@ -32,6 +43,7 @@ import selectivenet_for_semantic_segmentation_binary_amd as S  # noqa: E402
 import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd import _lib as K  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd import parallel  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch  # noqa: E402
 
 TRAIN_GFLOP_PER_IMG_256 = 220.38  # fwd 73.535 x 3 - first-layer dgrad
@@ -46,28 +58,40 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128, help="global batch (split over ranks)")
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="fp32", help="headline configuration")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the extra bf16 measurement")
+    ap.add_argument("--selective", type=int, default=1, help="0: non-selective UNet_B (BASELINE configs[1])")
     ap.add_argument("--lamb", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--kernel-steps", type=int, default=3, help="steps of the per-kernel attribution pass")
+    ap.add_argument("--no-full-loop", action="store_true")
     ap.add_argument("--layer-report", action="store_true", help="print per-entry-point timing to stderr")
     return ap.parse_args()
 
 
+def _i(v):
+    return int(getattr(v, "value", v))
+
+
 class KernelTimer:
-    """Brackets the MFMA GEMM entry points with HIP events on the launch stream (torch's current
+    """Brackets the kernel entry points with HIP events on the launch stream (torch's current
     stream, the one the kernels are launched on) and attributes each launch to the kernel it
-    dispatches to (selunet_gemm_kernel_name), with its algorithmic FLOPs (2*M*N*K of the true,
-    unpadded GEMM) and algorithmic HBM bytes (each operand tensor read once, output written once)."""
+    dispatches to, with its algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM) and algorithmic
+    HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
-    ENTRY = ("selunet_gemm_gather", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws")
+    MFMA = ("selunet_gemm_gather", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
+    HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_maxpool2_fwd",
+           "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
 
-    def __init__(self, esz):
+    def __init__(self, esz, tag):
         self.active = False
         self.esz = esz
+        self.tag = tag
         self.rec = {}  # kernel name -> list of (start, end, flops, bytes)
+        self.bound = {}
         self.shapes = {}  # (kernel name, operand shape) -> list of (start, end, flops)
 
     @staticmethod
@@ -79,29 +103,63 @@ class KernelTimer:
         return sum(g.n * hs * ws * g.src[i].channels * (4 if g.src[i].layout == 1 else self.esz)
                    for i in range(g.nsrc))
 
-    def __call__(self, name, args, fn):
-        if not self.active or name not in self.ENTRY:
-            return fn()
+    def _describe(self, name, args):
+        esz, t = self.esz, self.tag
         if name == "selunet_gemm_gather":
-            g, n_cols, mode = args[0], args[2], args[4].mode
-            kname = K.query("selunet_gemm_kernel_name", g, None, n_cols, mode, args[5]).decode()
+            g, n_cols, mode = args[0], _i(args[2]), args[4].mode
+            kname = K.query("selunet_gemm_kernel_name", g, None, n_cols, mode, _i(args[5])).decode()
             m = g.n * g.h * g.w
             flops = 2.0 * m * n_cols * self._k(g)
-            nbytes = self._src_bytes(g) + m * n_cols * self.esz + n_cols * self._k(g) * self.esz
-            shape = f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
-        else:
+            nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
+            return kname, "mfma", flops, nbytes, f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
+        if name in ("selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to"):
             gp, gq = args[0], args[1]
-            dt = args[3] if name == "selunet_gemm_wgrad" else args[5]
+            dt = _i(args[{"selunet_gemm_wgrad": 3, "selunet_gemm_wgrad_ws": 5, "selunet_gemm_wgrad_ws_to": 7}[name]])
             kname = K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, dt).decode()
-            if name == "selunet_gemm_wgrad_ws" and args[4] > 0:
+            if name != "selunet_gemm_wgrad" and _i(args[4]) > 0:
                 kname += "+reduce"  # (the entry point's time includes the split reduction)
             flops = 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
-            shape = f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
+            return kname, "mfma", flops, nbytes, f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
+        if name == "selunet_first_conv_fwd":  # (x, n, cin, h, w, wpack, y, stats, dtype, stream)
+            n, cin, h, w = (_i(a) for a in args[1:5])
+            m = n * h * w
+            return (f"first_conv_fwd<{t}>", "hbm", 2.0 * m * 64 * 9 * cin, m * cin * 4 + m * 64 * esz,
+                    f"first fwd {h}x{w}")
+        if name == "selunet_first_conv_wgrad":  # (x, n, cin, h, w, dy, slab, dtype, stream)
+            n, cin, h, w = (_i(a) for a in args[1:5])
+            m = n * h * w
+            return (f"first_conv_wgrad<{t}>", "hbm", 2.0 * m * 64 * 9 * cin, m * cin * 4 + m * 64 * esz,
+                    f"first wgrad {h}x{w}")
+        if name == "selunet_bn_bwd_apply":  # (dA, y, M, C, ...): read dA + y, write dy
+            m, c = _i(args[2]), _i(args[3])
+            return f"bn_bwd_apply<{t}>", "hbm", 0.0, 3 * m * c * esz, f"bn_bwd_apply C={c}"
+        if name == "selunet_maxpool2_fwd":  # (y, n, h, w, c, ...): read y, write y/4
+            n, h, w, c = (_i(a) for a in args[1:5])
+            return f"maxpool2_fwd<{t}>", "hbm", 0.0, 1.25 * n * h * w * c * esz, f"pool fwd {h}x{w} C={c}"
+        if name == "selunet_maxpool2_bwd":  # (y, n, h, w, c, sc, sh, dp, dskip, dz, ...)
+            n, h, w, c = (_i(a) for a in args[1:5])
+            m = n * h * w
+            skip = args[8] is not None and _i(args[8]) != 0
+            return (f"maxpool2_bwd<{t}>", "hbm", 0.0, (2.25 + (1 if skip else 0)) * m * c * esz,
+                    f"pool bwd {h}x{w} C={c}")
+        if name == "selunet_heads_fwd":  # (y, M, sc, sh, w, b, nheads, o0, o1, o2, ...)
+            m, nh = _i(args[1]), _i(args[6])
+            return f"heads_fwd<{t}>", "hbm", 2.0 * m * 64 * nh, m * 64 * esz + nh * m * 4, "heads fwd"
+        if name == "selunet_heads_bwd":  # (y, M, sc, sh, w, nheads, g0, g1, g2, dz, ...)
+            m, nh = _i(args[1]), _i(args[5])
+            return f"heads_bwd<{t}>", "hbm", 4.0 * m * 64 * nh, 2 * m * 64 * esz + nh * m * 4, "heads bwd"
+        return None
+
+    def __call__(self, name, args, fn):
+        if not self.active or (name not in self.MFMA and name not in self.HBM):
+            return fn()
+        kname, bound, flops, nbytes, shape = self._describe(name, args)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         rc = fn()
         e.record()
+        self.bound[kname] = bound
         self.rec.setdefault(kname, []).append((s, e, flops, nbytes))
         self.shapes.setdefault((kname, shape), []).append((s, e, flops))
         return rc
@@ -118,7 +176,8 @@ class KernelTimer:
         out = {}
         for k, lst in self.rec.items():
             out[k] = {"ms": sum(s.elapsed_time(e) for s, e, _, _ in lst), "launches": len(lst),
-                      "flops": sum(f for _, _, f, _ in lst), "bytes": sum(b for _, _, _, b in lst)}
+                      "flops": sum(f for _, _, f, _ in lst), "bytes": sum(b for _, _, _, b in lst),
+                      "bound": self.bound[k]}
         return out
 
 
@@ -132,6 +191,17 @@ def load_traffic(kernel):
         if kernel in d.get("kernels", {}):
             return d["kernels"][kernel], os.path.relpath(path, REPO)
     return None, None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(args):
@@ -151,10 +221,149 @@ def cpu_baseline(args):
         O.train_step(params, buffers, opt, xt, lt, True, lamb=args.lamb)
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_batch * args.cpu_steps / dt, 4), "unit": "images/s", "cores": cores,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of the oracle train step, SelectiveUNet_B "
                       f"bs={args.cpu_batch} {args.size}x{args.size} fp32, torch {torch.__version__} CPU, "
-                      f"{cores} threads; {dt:.1f} s"}
+                      f"{cores} threads of {cpu_model()}; {dt:.1f} s"}
+
+
+def timed(fn, steps, world, dev):
+    """Run fn `steps` times between barrier + synchronize brackets; max over ranks (seconds)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def run_config(args, dtype, world, rank, dev, xt, lt, local_batch):
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    selective = bool(args.selective)
+    net = S.UNet_B("RGB", selective=selective, compute_dtype=dt)
+    p = L.seeded_params(0, "RGB", selective, bn_affine_random=False)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    net = net.to(dev).train()
+    parallel.broadcast_params(net)
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    loss_a = S.BCEWithLogitsLoss()
+    state = {}
+
+    def step():
+        if selective:
+            out, sel, aux = net(xt)
+            loss = loss_a(aux, lt)
+            sel_loss, _ = S.calc_selective_risk_image_b(out, sel, target=lt, lamb=args.lamb)
+            loss = loss + sel_loss
+        else:
+            out, sel = net(xt), None
+            loss = loss_a(out, lt)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        state["loss"], state["out"], state["sel"] = loss, out, sel
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed(step, args.steps, world, dev)
+    final_loss = float(state["loss"].item())
+    res = {"value": round(args.batch * args.steps / elapsed, 2), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+           "final_loss": round(final_loss, 5)}
+
+    # per-kernel attribution: its own pass, so the headline steps carry no event records
+    if not args.no_kernel_timing:
+        timer = KernelTimer(2 if dt == torch.bfloat16 else 4, "bf16" if dt == torch.bfloat16 else "f32")
+        K.set_call_hook(timer)
+        timer.active = True
+        ksteps = max(1, args.kernel_steps)
+        kel = timed(step, ksteps, world, dev)
+        timer.active = False
+        K.set_call_hook(None)
+        res["roofline"] = roofline(args, dtype, timer, ksteps, kel, local_batch)
+        if args.layer_report and rank == 0:
+            for ms, k, shape, n, tf in timer.shape_summary(ksteps):
+                print(f"[{dtype}] {ms:7.3f} ms/step {n:2d}x {tf:7.1f} TF/s  {k:30s} {shape}", file=sys.stderr)
+
+    # full training-loop iteration: step + on-device metrics and loss sums (train.py:194-241)
+    if not args.no_full_loop:
+        ev = SegMetrics(dev, selective=selective, rule="train")
+        sums = torch.zeros(3, dtype=torch.float64, device=dev)
+
+        def loop_step():
+            loss = step()
+            sums[0] += loss.detach()
+            ev.add_batch(state["out"].detach(), lt, None if state["sel"] is None else state["sel"].detach())
+
+        def loop(nsteps):
+            for _ in range(nsteps):
+                loop_step()
+            ev.raw()  # the per-epoch read-back (all-reduced over ranks)
+            sums.cpu()
+
+        loop(1)
+        el = timed(lambda: loop(args.steps), 1, world, dev)
+        res["full_loop"] = {"value": round(args.batch * args.steps / el, 2), "ms_per_step": round(1e3 * el / args.steps, 3),
+                            "includes": "step + SegMetrics.add_batch (thresholded masks, 2x2 confusion matrix, "
+                                        "rejection counts) + loss sums, read back once"}
+    res["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+    del net, opt, state, step
+    gc.collect()
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
+    return res
+
+
+def roofline(args, dtype, timer, ksteps, kel, local_batch):
+    ksum = timer.summary()
+    if not ksum:
+        return None
+    mfma_peak, mfma_unit = PEAK[dtype]
+
+    def frac(v):
+        if v["ms"] <= 0:
+            return 0.0, 0.0
+        if v["bound"] == "mfma":
+            a = v["flops"] / (v["ms"] * 1e-3) / 1e12
+            return a, a / mfma_peak
+        a = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+        return a, a / HBM_PEAK_GBS
+
+    dom = max(ksum, key=lambda n: ksum[n]["ms"])
+    d = ksum[dom]
+    achieved, fr = frac(d)
+    launches = max(1, d["launches"])
+    # the committed PMC summary was collected on the default workload (bs=128 per GPU, 256x256)
+    traffic, tsrc = load_traffic(dom) if (args.size, local_batch) == (256, 128) else (None, None)
+    hbm = d["bound"] == "hbm"
+    return {
+        "bound": d["bound"], "kernel": dom, "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS if hbm else mfma_peak, "unit": "GB/s" if hbm else mfma_unit, "frac": round(fr, 4),
+        "traffic": traffic["hbm_bytes_per_launch"] if traffic else None, "traffic_source": tsrc,
+        "algorithmic_flops_per_launch": d["flops"] / launches, "algorithmic_bytes_per_launch": d["bytes"] / launches,
+        "per_launch_ms": round(d["ms"] / launches, 4), "launches": d["launches"],
+        "kernel_share_of_step": round(d["ms"] / (kel * 1e3), 4),
+        "timing": f"HIP events on the launch stream, separate {ksteps}-step pass after the headline timing",
+        "all": {n: {"bound": v["bound"], "ms_per_step": round(v["ms"] / ksteps, 3),
+                    "launches_per_step": v["launches"] // ksteps,
+                    "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] else 0.0,
+                    "hbm_gbs_algorithmic": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else 0.0,
+                    "frac": round(frac(v)[1], 4)}
+                for n, v in sorted(ksum.items(), key=lambda kv: -kv[1]["ms"])},
+    }
 
 
 def main():
@@ -166,17 +375,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         parallel.init_data_parallel(backend="nccl")
-    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-
-    net = S.UNet_B("RGB", selective=True, compute_dtype=dt)
-    p = L.seeded_params(0, "RGB", True, bn_affine_random=False)
-    with torch.no_grad():
-        for k, t in net.named_parameters():
-            t.copy_(torch.tensor(p[k]))
-    net = net.to(dev).train()
-    parallel.broadcast_params(net)
-    opt = S.Adam(net.parameters(), lr=1e-3)
-    loss_a = S.BCEWithLogitsLoss()
+        # the per-kernel event records add host work to the small per-GPU steps of the scaling runs
+        args.no_kernel_timing = True
 
     x, lab = make_batch(args.batch, args.size, seed=0)
     lo, hi = parallel.chunk_bounds(args.batch, rank, world)
@@ -185,95 +385,43 @@ def main():
     lt = torch.tensor(lab[lo:hi], device=dev)
     del x, lab
 
-    timer = KernelTimer(2 if dt == torch.bfloat16 else 4)
-    # per-kernel HIP-event timing (the roofline object) at N = 1; multi-GPU lines skip it, so the
-    # event records add no host work to the small per-GPU steps of the scaling runs
-    if world > 1:
-        args.no_kernel_timing = True
-    if not args.no_kernel_timing:
-        K.set_call_hook(timer)
+    head = run_config(args, args.dtype, world, rank, dev, xt, lt, hi - lo)
+    extra = None
+    if args.dtype == "fp32" and not args.no_bf16:
+        extra = run_config(args, "bf16", world, rank, dev, xt, lt, hi - lo)
 
-    def step():
-        out, sel, aux = net(xt)
-        aux_loss = loss_a(aux, lt)
-        sel_loss, cov = S.calc_selective_risk_image_b(out, sel, target=lt, lamb=args.lamb)
-        loss = aux_loss + sel_loss
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        return loss
-
-    for _ in range(args.warmup):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timer.active = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    timer.active = False
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    final_loss = float(loss.item())
-
-    value = args.batch * args.steps / elapsed
-    ms_step = 1e3 * elapsed / args.steps
-    roof = None
-    ksum = timer.summary() if not args.no_kernel_timing else None
-    if ksum:
-        dom = max(ksum, key=lambda n: ksum[n]["ms"])
-        d = ksum[dom]
-        peak, unit = PEAK[args.dtype]
-        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12 if d["ms"] > 0 else 0.0
-        launches = max(1, d["launches"])
-        # the committed PMC summary was collected on the default workload (bs=128 per GPU, 256x256);
-        # its per-launch bytes describe other shapes' launches not at all
-        traffic, tsrc = load_traffic(dom) if (args.size, hi - lo) == (256, 128) else (None, None)
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 4),
-                "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
-                "traffic_source": tsrc,
-                "algorithmic_flops_per_launch": d["flops"] / launches,
-                "algorithmic_bytes_per_launch": d["bytes"] / launches,
-                "per_launch_ms": round(d["ms"] / launches, 4),
-                "launches": d["launches"], "kernel_share_of_step": round(d["ms"] / (elapsed * 1e3), 4),
-                "all": {n: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] // args.steps,
-                            "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] else 0.0,
-                            "hbm_gbs_algorithmic": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else 0.0}
-                        for n, v in sorted(ksum.items(), key=lambda kv: -kv[1]["ms"])}}
-        if args.layer_report and rank == 0:
-            for ms, k, shape, n, tf in timer.shape_summary(args.steps):
-                print(f"{ms:7.3f} ms/step {n:2d}x {tf:7.1f} TF/s  {k:26s} {shape}", file=sys.stderr)
-    whole = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * value / 1e3  # TFLOP/s whole step
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
     if rank == 0:
+        value = head["value"]
+        whole = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * value / 1e3  # TFLOP/s whole step
+        model = "SelectiveUNet_B" if args.selective else "UNet_B"
+        what = f"selective_loss s_lamb={args.lamb:g}" if args.selective else "BCEWithLogits"
         line = {
-            "metric": f"train images/sec, SelectiveUNet_B {args.size}x{args.size} bs={args.batch} (global), "
-                      f"selective_loss s_lamb={args.lamb:g}",
-            "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
+            "metric": f"train images/sec, {model} {args.size}x{args.size} bs={args.batch} (global), {what}",
+            "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32" if args.dtype == "fp32" else "bf16",
             "data": f"synthetic (seeded tumor/benign {args.size}x{args.size} patches, HBM-resident)",
-            "config": {"workload": f"SelectiveUNet_B train step, global bs={args.batch}, {args.size}x{args.size}, "
-                                   f"Adam lr=1e-3, s_lamb={args.lamb:g}", "model": "SelectiveUNet_B",
-                       "global_batch": args.batch, "per_gpu_batch": hi - lo, "image": args.size,
-                       "parallelism": f"dp{world}"},
+            "config": {"workload": f"{model} train step, global bs={args.batch}, {args.size}x{args.size}, "
+                                   f"Adam lr=1e-3" + (f", s_lamb={args.lamb:g}" if args.selective else ""),
+                       "model": model, "global_batch": args.batch, "per_gpu_batch": hi - lo, "image": args.size,
+                       "parallelism": f"dp{world}",
+                       "arithmetic": "fp32 operands, exact fp32 MFMA products, fp32 accumulation"
+                       if args.dtype == "fp32" else "bf16 operands, fp32 accumulation"},
+            "gpu": torch.cuda.get_device_name(dev),
             "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
-            "final_loss": round(final_loss, 5),
-            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
-            "roofline": roof, "cpu_baseline": cpu,
+            "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
+            "full_loop": head.get("full_loop"),
+            "roofline": head.get("roofline"), "cpu_baseline": cpu,
         }
+        if extra is not None:
+            wb = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * extra["value"] / 1e3
+            extra["step_tflops"] = round(wb, 2)
+            extra["step_mfma_frac"] = round(wb / world / PEAK["bf16"][0], 4)
+            extra["note"] = "bf16 speed configuration (bf16 operands, fp32 accumulation); parity gates in DESIGN.md §4"
+            line["bf16"] = extra
         print(json.dumps(line))
     if world > 1:
         dist.barrier()
