@@ -952,17 +952,28 @@ conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out,
     const bool more = pt + 1 < (int)pt_end;
     load_tile(more ? pt + 1 : pt);
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
-#pragma unroll 1
-    for (int ks = 0; ks < WPIXT / 2; ++ks) {
+    // operands of k-step ks + 1 are read while k-step ks multiplies (the last step re-reads step 0:
+    // valid addresses, unused)
+    struct Frag {
+      float a, b[NTAP];
+    };
+    auto frag = [&](int ks) __attribute__((always_inline)) {
+      Frag f;
       const int p = 2 * ks + half;                        // k = pixel of this lane's half
-      const float a = pcol[p * BI];
+      f.a = pcol[p * BI];
       const int hbase = ((p / WTW) * WHW + p % WTW) * CJ;  // halo pixel of tap (0, 0)
-      float b[NTAP];
 #pragma unroll
-      for (int t = 0; t < NTAP; ++t) b[t] = xcol[hbase + toff[t]];
+      for (int t = 0; t < NTAP; ++t) f.b[t] = xcol[hbase + toff[t]];
+      return f;
+    };
+    Frag cur = frag(0);
+#pragma unroll 2
+    for (int ks = 0; ks < WPIXT / 2; ++ks) {
+      const Frag nxt = frag(ks + 1 < WPIXT / 2 ? ks + 1 : 0);
 #pragma unroll
       for (int t = 0; t < NTAP; ++t)
-        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[t], acc[t], 0, 0, 0);
+        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a, cur.b[t], acc[t], 0, 0, 0);
+      cur = nxt;
     }
     __syncthreads();  // every wave is done reading the tile
     if (more) {

@@ -975,16 +975,21 @@ __device__ __forceinline__ float ce_pixel(const float* __restrict__ x, int64_t b
     se += e[c];
   }
   inv_se = 1.0f / se;
-  float xt = xv[0];
+  float xt = t < 0 ? __builtin_nanf("") : xv[0];
 #pragma unroll
   for (int c = 1; c < 8; ++c) xt = c == t ? xv[c] : xt;
   return mx + __logf(se) - xt;
 }
 
+// class index of pixel i, or -1 outside [0, C): such a target (e.g. torch's ignore_index -100, or
+// an unconverted 0/255 mask) makes the pixel's loss term and gradients NaN — torch's
+// CrossEntropyLoss and the reference's scatter_ one-hot reject it — instead of being trained as
+// a clamped class
 __device__ __forceinline__ int ce_target(const int64_t* tgt, int64_t i, int C) {
   const int64_t t = tgt[i];
-  return (int)(t < 0 ? 0 : (t >= C ? C - 1 : t));
+  return (t < 0 || t >= C) ? -1 : (int)t;
 }
+__device__ __forceinline__ float ce_onehot(int c, int t) { return t < 0 ? __builtin_nanf("") : (c == t ? 1.0f : 0.0f); }
 
 __global__ void ce_selective_partials_kernel(const float* __restrict__ out, const float* __restrict__ sel,
                                              const int64_t* __restrict__ tgt, int64_t P, int C, int64_t hw,
@@ -1024,7 +1029,7 @@ __global__ void ce_selective_bwd_kernel(const float* __restrict__ out, const flo
     const float k = gl * s * inv_s0;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (c < C) d_out[base + c * hw] = k * (e[c] * inv_se - (c == t ? 1.0f : 0.0f));
+      if (c < C) d_out[base + c * hw] = k * (e[c] * inv_se - ce_onehot(c, t));
     const float ds = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
     d_sel[s1i] = ds;
     d_sel[s0i] = -ds;
@@ -1056,7 +1061,7 @@ __global__ void ce_bwd_kernel(const float* __restrict__ a, const int64_t* __rest
     ce_pixel(a, base, hw, C, t, e, inv_se);
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (c < C) d[base + c * hw] = g * (e[c] * inv_se - (c == t ? 1.0f : 0.0f));
+      if (c < C) d[base + c * hw] = g * (e[c] * inv_se - ce_onehot(c, t));
   }
 }
 

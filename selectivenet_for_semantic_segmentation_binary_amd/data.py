@@ -89,7 +89,12 @@ def construct_test(data_dir, test_fold=1):
 def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=True) -> PatchSet:
     """Decode (input .jpg, label .png) pairs of `{data_dir}/{patch_mag}x_{patch_size}/` once
     (PIL, as PatchDataset.__getitem__, utils/data_utils.py:209-217) into uint8 arrays; with
-    cache=True they are stored as .npy next to the patches and memory-mapped on later runs."""
+    cache=True they are stored as .npy next to the patches and memory-mapped on later runs.
+
+    Under data parallelism (one process per GPU, `train.py --local_rank ...`) only rank 0 decodes:
+    it writes each cache file under a temporary name and renames it into place (os.replace is
+    atomic, so no rank can map a half-written file), all ranks meet at a barrier, and every rank
+    then memory-maps the finished cache — one decoded copy on the host instead of one per GPU."""
     from PIL import Image
 
     root = os.path.join(data_dir, f"{patch_mag}x_{patch_size}")
@@ -101,7 +106,13 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
     cdir = os.path.join(root, "_selunet_cache")
     fi, fl = os.path.join(cdir, f"{key}_images.npy"), os.path.join(cdir, f"{key}_labels.npy")
     ids = [a.split("_input")[0] for a, _ in pairs]
+    shared = cache and parallel.is_initialized() and parallel.world_size() > 1
+    if shared and parallel.rank() != 0:
+        torch.distributed.barrier()  # rank 0 has written (or found) the cache
+        return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     if cache and os.path.exists(fi) and os.path.exists(fl):
+        if shared:
+            torch.distributed.barrier()
         return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     imgs = np.empty((len(pairs), patch_size, patch_size, 3), np.uint8)
     labs = np.empty((len(pairs), patch_size, patch_size), np.uint8)
@@ -110,8 +121,12 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
         labs[i] = np.array(Image.open(os.path.join(root, b)).convert("L"))
     if cache:
         os.makedirs(cdir, exist_ok=True)
-        np.save(fi, imgs)
-        np.save(fl, labs)
+        for path, arr in ((fi, imgs), (fl, labs)):
+            tmp = f"{path[:-4]}.tmp{os.getpid()}.npy"
+            np.save(tmp, arr)
+            os.replace(tmp, path)
+    if shared:
+        torch.distributed.barrier()
     return PatchSet(imgs, labs, ids)
 
 

@@ -254,7 +254,9 @@ class _CrossEntropyMean(torch.autograd.Function):
 
 class CrossEntropyLoss(nn.Module):
     """torch.nn.CrossEntropyLoss() with the defaults the reference uses (train.py:80): mean over
-    pixels, (N, C, H, W) logits, (N, H, W) int64 targets, no weights / ignore_index / smoothing."""
+    pixels, (N, C, H, W) logits, (N, H, W) int64 targets, no weights / smoothing. A target outside
+    [0, C) (torch's ignore_index pixels included) makes the loss and its gradient NaN rather than
+    being clamped into a class."""
 
     def __init__(self, weight=None, size_average=None, ignore_index=-100, reduce=None, reduction="mean",
                  label_smoothing=0.0):
@@ -262,6 +264,9 @@ class CrossEntropyLoss(nn.Module):
         if weight is not None or size_average is not None or reduce is not None or reduction != "mean" \
                 or label_smoothing != 0.0:
             raise NotImplementedError("only the reference's CrossEntropyLoss() (mean, unweighted) is implemented")
+        if ignore_index != -100:
+            raise NotImplementedError("ignore_index: the reference's labels are class indices 0..C-1 only "
+                                      "(utils/data_utils.py:220-221); targets outside [0, C) give a NaN loss")
         self.ignore_index = ignore_index
 
     def forward(self, input, target):

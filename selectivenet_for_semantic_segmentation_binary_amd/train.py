@@ -87,24 +87,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def spawn(argv, gpu_ids):
+def spawn(argv, gpu_ids, command=None):
     """One child process per listed GPU id (replaces torch.nn.DataParallel(device_ids=rank),
-    train.py:131-134). The parent never touches the GPU; it waits and returns the worst exit code."""
+    train.py:131-134). The parent never touches the GPU; it waits and returns the worst exit code.
+    command: the child command line (default: this module with `argv`)."""
     port = str(_free_port())
     procs = []
+    cmd = command or [sys.executable, "-m", __spec__.name if __spec__ else __name__, *argv]
     for r, gid in enumerate(gpu_ids):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(len(gpu_ids)),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port, SELUNET_GPU_ID=str(gid))
-        procs.append(subprocess.Popen([sys.executable, "-m", __spec__.name if __spec__ else __name__, *argv],
-                                      env=env))
+        procs.append(subprocess.Popen(cmd, env=env))
     rc = 0
     try:
-        for p in procs:
-            rc = max(rc, p.wait())
-            if rc:
-                for q in procs:
-                    if q.poll() is None:
+        # poll every child: the first non-zero exit (of any rank, not just the next one in order)
+        # ends the job at once instead of leaving the others blocked in a collective until the
+        # process-group timeout
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                rc = max(rc, code) if code >= 0 else max(rc, 128 - code)
+                if code != 0:
+                    for q in live:
                         q.terminate()
+            time.sleep(0.2)
     finally:
         for q in procs:
             if q.poll() is None:

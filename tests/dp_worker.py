@@ -4,7 +4,8 @@ Runs the golden fixture's training steps exactly as a `--gpus N` job would (trai
 with DataParallel replaced by one process per rank): the rank takes its contiguous chunk of the
 batch, runs the MI355X UNet_B / selective loss / BCE / Adam, with the loss partial sums and the
 gradients all-reduced by `parallel`. Rank r writes its results to OUT/r{r}_s{step}.npz.
-All ranks share cuda:0 over a `gloo` group here (one-GPU box); `bench.py --gpus N` uses RCCL.
+Backend "gloo": all ranks share cuda:0 (one-GPU box). Backend "nccl" (RCCL over xGMI): rank r
+runs on cuda:r, as `bench.py --gpus N` and `train.py --local_rank ...` do.
 """
 import os
 import sys
@@ -19,9 +20,10 @@ from tests import _golden as G
 from tests.test_gpu_model import build
 
 
-def main(fname, out):
-    rank, world = parallel.init_data_parallel("gloo")
-    torch.cuda.set_device(0)
+def main(fname, out, backend="gloo"):
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local if backend == "nccl" else 0)
+    rank, world = parallel.init_data_parallel(backend)
     d = G.load(fname)
     n, size, selective = int(d["meta_n"]), int(d["meta_size"]), bool(d["meta_selective"])
     assert world == int(d["meta_chunks"]), (world, int(d["meta_chunks"]))
@@ -41,7 +43,9 @@ def main(fname, out):
         loss = aux_loss + select_loss
         opt.zero_grad()
         loss.backward()
-        res = {"loss": loss.item(), "coverage": coverage.item(), "output": o.detach().cpu().numpy()}
+        res = {"loss": loss.item(), "coverage": coverage.item(), "aux_loss": aux_loss.item(),
+               "select_loss": select_loss.item(), "output": o.detach().cpu().numpy(),
+               "selection": sel.detach().cpu().numpy(), "aux": aux.detach().cpu().numpy()}
         if rank == 0:
             for k, p in net.named_parameters():
                 res["grad/" + k] = p.grad.detach().cpu().numpy()
@@ -58,4 +62,4 @@ def main(fname, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *sys.argv[3:4])

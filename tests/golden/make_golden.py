@@ -23,6 +23,7 @@ from collections import OrderedDict
 
 import numpy as np
 import torch
+import torch.utils.checkpoint
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -57,10 +58,30 @@ def build_ref(seed, selective, input_type="RGB"):
     return net
 
 
-def sample_idx(name, numel):
+def sample_idx(name, numel, k=N_SAMPLES):
     h = int(hashlib.sha1(name.encode()).hexdigest()[:8], 16)
     rng = np.random.Generator(np.random.PCG64(h))
-    return np.sort(rng.choice(numel, size=min(N_SAMPLES, numel), replace=False))
+    return np.sort(rng.choice(numel, size=min(k, numel), replace=False))
+
+
+class _Checkpointed(torch.nn.Module):
+    """Runs one of the reference's own sub-modules under torch.utils.checkpoint: only its input is
+    kept for the backward and the module is re-run there (memory for batch 128 at 256x256 on the
+    64 GB build container). The arithmetic is the module's own; the re-run's BatchNorm
+    running-statistic update is undone by the caller (ref_step restores the buffers)."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+
+    def forward(self, x):
+        return torch.utils.checkpoint.checkpoint(self.m, x, use_reentrant=False)
+
+
+def checkpoint_modules(net):
+    for name, m in list(net.named_children()):
+        net._modules[name] = _Checkpointed(m)
+    return net
 
 
 def record_tensors(out, prefix, named, full_max=1024):
@@ -75,15 +96,18 @@ def record_tensors(out, prefix, named, full_max=1024):
             out[f"{prefix}val/{k}"] = a[idx]
 
 
-def ref_step(net, optim, x, lab, selective, lamb, chunks=1):
-    """train.py:194-209 (selective / non-selective), with optional DataParallel emulation."""
+def ref_step(net, optim, x, lab, selective, lamb, chunks=1, ckpt=False, names=None):
+    """train.py:194-209 (selective / non-selective), with optional DataParallel emulation.
+    ckpt: the network's sub-modules are checkpointed (checkpoint_modules); their BN buffers are
+    restored to the forward's values after the backward's re-run. names: parameter -> reference
+    name (the checkpoint wrappers change named_parameters)."""
     loss_A = torch.nn.BCEWithLogitsLoss()
     xs = torch.chunk(x, chunks) if chunks > 1 else [x]
     outs, saved = [], None
     for r, xc in enumerate(xs):
         o = net(xc)
         outs.append(o if selective else (o,))
-        if chunks > 1 and r == 0:
+        if (chunks > 1 or ckpt) and r == 0:
             saved = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
     res = {}
     output = torch.cat([o[0] for o in outs])
@@ -103,7 +127,8 @@ def ref_step(net, optim, x, lab, selective, lamb, chunks=1):
         sd = net.state_dict()  # autograd version-checks the buffers BN read)
         for k, v in saved.items():
             sd[k].copy_(v)
-    grads = OrderedDict((n, p.grad.detach().clone()) for n, p in net.named_parameters())
+    named = [(names[id(p)] if names else n, p) for n, p in net.named_parameters()]
+    grads = OrderedDict((n, p.grad.detach().clone()) for n, p in named)
     optim.step()
     res.update(output=output.detach(), loss=loss.detach(), grads=grads)
     return res
@@ -129,22 +154,31 @@ def fp64_truth(out, n, size, selective, lamb, chunks, seed, data_seed):
             out[f"s0/grad64val/{k}"] = a[out[f"s0/gradidx/{k}"]]
 
 
-def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outputs=True, seed=0, data_seed=1):
+def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outputs=True, seed=0, data_seed=1,
+                 fp64=True, ckpt=False, out_samples=N_SAMPLES, mask_bits=False):
+    """ckpt: checkpointed sub-modules (large batches); fp64: also record the fp64 step-0 truth;
+    out_samples: logits sampled per head when full_outputs is False; mask_bits: also store the
+    output head's training-rule mask as packed bits (flip counting at full size)."""
     x, lab = make_batch(n, size, seed=data_seed)
     xt, lt = torch.tensor(x), torch.tensor(lab)
+    del x
     torch.manual_seed(0)
     net = build_ref(seed, selective)
+    names = None
+    if ckpt:
+        names = {id(p): k for k, p in net.named_parameters()}
+        checkpoint_modules(net)
     net.train()
     optim = torch.optim.Adam(net.parameters(), lr=1e-3, weight_decay=0)
     out = {"meta_n": n, "meta_size": size, "meta_selective": int(selective), "meta_lamb": lamb,
            "meta_steps": steps, "meta_chunks": chunks, "meta_seed": seed, "meta_data_seed": data_seed}
-    out["x_sha1"] = np.bytes_(hashlib.sha1(x.tobytes()).hexdigest())
+    out["x_sha1"] = np.bytes_(hashlib.sha1(xt.numpy().tobytes()).hexdigest())
     out["label_sha1"] = np.bytes_(hashlib.sha1(lab.tobytes()).hexdigest())
     if full_outputs and n * size * size <= 65536:  # inputs are regenerated from the seed for big batches
-        out["x"] = x
+        out["x"] = xt.numpy()
         out["label"] = lab
     for s in range(steps):
-        r = ref_step(net, optim, xt, lt, selective, lamb, chunks)
+        r = ref_step(net, optim, xt, lt, selective, lamb, chunks, ckpt=ckpt, names=names)
         pre = f"s{s}/"
         for k in ("loss", "aux_loss", "select_loss", "coverage"):
             if k in r:
@@ -156,7 +190,7 @@ def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outp
                 out[pre + h] = a
             else:
                 flat = a.ravel()
-                idx = sample_idx(h, flat.size)
+                idx = sample_idx(h, flat.size, out_samples)
                 out[pre + h + "_idx"] = idx
                 out[pre + h + "_val"] = flat[idx]
                 out[pre + h + "_sum"] = np.float64(a.astype(np.float64).sum())
@@ -164,13 +198,26 @@ def step_fixture(fname, n, size, selective, lamb=2, steps=2, chunks=1, full_outp
             mask = (1.0 * (1 / (1 + np.exp(-a.astype("float64"))) > 0.5)).astype("uint8")  # train.py:150,153
             out[pre + h + "_mask_sha1"] = np.bytes_(hashlib.sha1(mask.tobytes()).hexdigest())
             out[pre + h + "_mask_count"] = np.int64(mask.sum())
+            # reference logits within 1e-6 of the decision boundary (a mask bit another fp32
+            # summation order may legitimately flip)
+            out[pre + h + "_near0_count"] = np.int64((np.abs(a) < 1e-6).sum())
+            out[pre + h + "_absmax"] = np.float64(np.abs(a).max())
+            if mask_bits and h == "output":
+                out[pre + h + "_mask_bits"] = np.packbits(mask.ravel())
         record_tensors(out, pre + "grad", r["grads"])
-        record_tensors(out, pre + "param", OrderedDict(net.named_parameters()))
-        bufs = OrderedDict((k, v) for k, v in net.state_dict().items() if "running" in k)
+        params = OrderedDict((names[id(p)] if names else k, p) for k, p in net.named_parameters())
+        record_tensors(out, pre + "param", params)
+        sd = net.state_dict()
+        bufs = OrderedDict((k.replace(".m.", ".") if ckpt else k, v) for k, v in sd.items())
         for k, v in bufs.items():
-            out[pre + "buf/" + k] = v.numpy().astype(np.float32)
-        out[pre + "num_batches_tracked"] = np.int64(net.state_dict()["encoder_layer_1_1.1.num_batches_tracked"].item())
-    fp64_truth(out, n, size, selective, lamb, chunks, seed, data_seed)
+            if "running" in k:
+                out[pre + "buf/" + k] = v.numpy().astype(np.float32)
+        nbt = [v for k, v in bufs.items() if k == "encoder_layer_1_1.1.num_batches_tracked"][0]
+        out[pre + "num_batches_tracked"] = np.int64(nbt.item())
+        del r
+    if fp64:
+        del net, optim
+        fp64_truth(out, n, size, selective, lamb, chunks, seed, data_seed)
     path = os.path.join(HERE, fname)
     np.savez_compressed(path, **out)
     print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB)")
@@ -462,7 +509,128 @@ def ce_step_fixture(fname, n, size, selective, lamb=2, steps=2, seed=0, data_see
     print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB): loss {out['s0/loss']:.6f}")
 
 
+def _perturbed(x, k):
+    """The input with a rounding-level relative perturbation (1e-7 * N(0, 1) per element, member k)."""
+    rng = np.random.Generator(np.random.PCG64(1000 + k))
+    return (x.astype(np.float64) * (1.0 + 1e-7 * rng.standard_normal(x.shape))).astype(np.float32)
+
+
+def _sampled(d, name, g):
+    a = g.detach().cpu().numpy().astype(np.float64).ravel()
+    if f"s0/gradfull/{name}" in d:
+        return a
+    return a[d[f"s0/gradidx/{name}"]]
+
+
+def augment_ensemble(fname, k_members=8, ckpt=False):
+    """How chaotic is the reference's own fp32 gradient? ReLU-mask and max-pool-argmax flips make
+    it a discontinuous function of rounding noise: re-run the reference step 0 on K copies of the
+    input perturbed at the rounding level (_perturbed) and record, per tensor, the largest
+    relative L2 error of those fp32 runs — against each member's own fp64 run when the fixture
+    has an fp64 truth (`s0/grad_ens/<name>`), otherwise against the unperturbed fp32 run
+    (`s0/grad_spread/<name>`). The parity tests bound the HIP path's error by this spread."""
+    path = os.path.join(HERE, fname)
+    d = dict(np.load(path, allow_pickle=False))
+    n, size = int(d["meta_n"]), int(d["meta_size"])
+    selective, lamb = bool(d["meta_selective"]), int(d["meta_lamb"])
+    chunks, seed = int(d.get("meta_chunks", 1)), int(d["meta_seed"])
+    x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
+    ce = "meta_n_cls" in d  # the CE UNet fixtures (ce_step_fixture)
+    if ce:
+        lab = lab.astype(np.int64)
+    has64 = any(k.startswith("s0/grad64norm/") for k in d)
+    names = [k[len("s0/gradnorm/"):] for k in d if k.startswith("s0/gradnorm/")]
+    worst = {nm: 0.0 for nm in names}
+    for k in range(1, k_members + 1):
+        xp = _perturbed(x, k)
+        runs = {}
+        for dt in ((torch.float32, torch.float64) if has64 else (torch.float32,)):
+            if ce:
+                net = build_ref_ce(seed, selective, int(d["meta_n_cls"])).to(dt).train()
+                optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+                r = ref_step_ce(net, optim, torch.tensor(xp, dtype=dt), torch.tensor(lab), selective, lamb)
+                runs[dt] = {nm: _sampled(d, nm, g) for nm, g in r["grads"].items()}
+                del net, optim, r
+                continue
+            net = build_ref(seed, selective)
+            pn = None
+            if ckpt:
+                pn = {id(p): q for q, p in net.named_parameters()}
+                checkpoint_modules(net)
+            net = net.to(dt).train()
+            optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+            r = ref_step(net, optim, torch.tensor(xp, dtype=dt), torch.tensor(lab, dtype=dt), selective, lamb, chunks,
+                         ckpt=ckpt, names=pn)
+            runs[dt] = {nm: _sampled(d, nm, g) for nm, g in r["grads"].items()}
+            del net, optim, r
+        for nm in names:
+            g32 = runs[torch.float32][nm]
+            ref = runs[torch.float64][nm] if has64 else (d[f"s0/gradfull/{nm}"] if f"s0/gradfull/{nm}" in d
+                                                          else d[f"s0/gradval/{nm}"]).astype(np.float64)
+            e = float(np.linalg.norm(g32 - ref) / max(np.linalg.norm(ref), 1e-30))
+            worst[nm] = max(worst[nm], e)
+        print(f"{fname}: member {k}/{k_members} done", flush=True)
+    key = "s0/grad_ens/" if has64 else "s0/grad_spread/"
+    for nm, e in worst.items():
+        d[key + nm] = np.float64(e)
+    d["meta_ens_members"] = np.int64(k_members)
+    np.savez_compressed(path, **d)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB) with the {k_members}-member perturbation ensemble")
+
+
+def check_checkpointing(n=2, size=32):
+    """The checkpointed reference step equals the plain one (same modules, same arithmetic)."""
+    x, lab = make_batch(n, size, seed=1)
+    res = []
+    for ckpt in (False, True):
+        net = build_ref(0, True)
+        names = {id(p): k for k, p in net.named_parameters()}
+        if ckpt:
+            checkpoint_modules(net)
+        net.train()
+        optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+        res.append(ref_step(net, optim, torch.tensor(x), torch.tensor(lab), True, 2, ckpt=ckpt, names=names))
+    a, b = res
+    assert a["loss"].item() == b["loss"].item()
+    for k in a["grads"]:
+        assert torch.equal(a["grads"][k], b["grads"][k]), k
+    print("checkpointed reference step == plain reference step (bitwise)")
+
+
+def big_fixtures():
+    """Full-size fixtures (BASELINE configs 3-5): batch 128 at 256x256 (fp32 only: the fp64 run
+    would need ~170 GB of host memory), the 16-image per-GPU shard of the 8-GPU run with its fp64
+    truth, and 512x512 at batch 2 with its fp64 truth."""
+    check_checkpointing()
+    step_fixture("step_sel_n16_256.npz", 16, 256, selective=True, lamb=2, steps=1, full_outputs=False,
+                 out_samples=8192, mask_bits=True, data_seed=7)
+    step_fixture("step_sel_n2_512.npz", 2, 512, selective=True, lamb=2, steps=1, full_outputs=False,
+                 out_samples=8192, mask_bits=True, data_seed=8)
+    step_fixture("step_sel_n128_256.npz", 128, 256, selective=True, lamb=2, steps=1, full_outputs=False,
+                 fp64=False, ckpt=True, out_samples=16384, mask_bits=True, data_seed=0)
+    big512()
+
+
+def big512():
+    """The 8-image per-GPU shard of configs[4] (512x512, batch 64 over 8 GPUs), fp32 reference."""
+    step_fixture("step_sel_n8_512.npz", 8, 512, selective=True, lamb=2, steps=1, full_outputs=False,
+                 fp64=False, ckpt=True, out_samples=16384, mask_bits=True, data_seed=9)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["big"]:
+        big_fixtures()
+        sys.exit(0)
+    if sys.argv[1:2] == ["ensemble"]:
+        for f in sys.argv[2:]:
+            augment_ensemble(f, k_members=8 if "n128" not in f else 3, ckpt="n128" in f or "n8_512" in f)
+        sys.exit(0)
+    if sys.argv[1:] == ["big512"]:
+        big512()
+        sys.exit(0)
+    if sys.argv[1:] == ["dp2"]:
+        step_fixture("dp_sel_n8_32_c2.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=2)
+        sys.exit(0)
     if sys.argv[1:] == ["miou"]:
         miou_fixture()
         sys.exit(0)
@@ -476,6 +644,7 @@ if __name__ == "__main__":
     step_fixture("step_nosel_n2_64.npz", 2, 64, selective=False, steps=2)
     step_fixture("step_sel_lamb8_n3_32.npz", 3, 32, selective=True, lamb=8, steps=1)
     step_fixture("dp_sel_n8_32_c4.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=4)
+    step_fixture("dp_sel_n8_32_c2.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=2)
     step_fixture("step_sel_n4_256.npz", 4, 256, selective=True, lamb=2, steps=1, full_outputs=True)
     eval_fixture("eval_sel_n4_64.npz")
     miou_fixture()

@@ -102,6 +102,25 @@ def test_ce_loss_kernels_against_torch(n, c, h, w):
         assert G.max_rel(a.grad.cpu().numpy(), b.grad.numpy()) < 1e-4
 
 
+@pytest.mark.parametrize("bad", [-100, 2, 255])
+def test_ce_out_of_range_target_is_not_clamped(bad):
+    """A target outside [0, C) (torch's ignore_index -100, an unconverted 255 mask value) is an
+    error in torch / the reference's one-hot; here it makes the loss and gradients NaN instead of
+    being trained as a clamped class."""
+    g = torch.Generator().manual_seed(1)
+    out = torch.randn(1, 2, 4, 4, generator=g).to(DEV).requires_grad_()
+    sel = torch.randn(1, 2, 4, 4, generator=g).to(DEV).requires_grad_()
+    lab = torch.zeros(1, 4, 4, dtype=torch.int64)
+    lab[0, 1, 2] = bad
+    l1 = S.CrossEntropyLoss()(out, lab.to(DEV))
+    l2, _ = S.calc_selective_risk_image(out, sel, lab.to(DEV), lamb=2)
+    (l1 + l2).backward()
+    assert torch.isnan(l1).item() and torch.isnan(l2).item()
+    assert torch.isnan(out.grad).any().item()
+    with pytest.raises(NotImplementedError):
+        S.CrossEntropyLoss(ignore_index=0)
+
+
 @pytest.mark.parametrize("n_cls,selective", [(3, False), (2, True)])
 def test_ce_unet_forward_bf16_and_classes(n_cls, selective):
     """Other class counts / bf16 through the N-output heads kernel vs the oracle (fp32 logits within

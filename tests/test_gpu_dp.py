@@ -1,7 +1,9 @@
-"""Multi-process data parallelism on the GPU against the reference's DataParallel fixture.
+"""Multi-process data parallelism on the GPU against the reference's DataParallel fixtures.
 
-4 ranks (tests/dp_worker.py, one process each, `gloo` group, all on cuda:0 of the one-GPU
-box) train on contiguous chunks of the 8-image batch; their concatenated logits, the global
+N ranks (tests/dp_worker.py, one process each) train on contiguous chunks of the 8-image batch:
+over a `gloo` group all on cuda:0 (runs on the one-GPU box), and over RCCL (`nccl`, rank r on
+cuda:r — the path bench.py --gpus N and train.py --local_rank take) whenever the box has at
+least N GPUs; their concatenated logits, the global
 loss/coverage every rank reports, the summed gradients and rank 0's parameters and BN buffers
 are compared with `dp_sel_n8_32_c4.npz` — the reference model run under DataParallel-chunk
 semantics over 4 replicas (tests/golden/make_golden.py) — with the same checks as the
@@ -28,8 +30,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_four_rank_dp_matches_dataparallel_fixture(tmp_path):
-    fname = "dp_sel_n8_32_c4.npz"
+def _gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.parametrize("fname,backend", [
+    ("dp_sel_n8_32_c4.npz", "gloo"),
+    pytest.param("dp_sel_n8_32_c2.npz", "nccl",
+                 marks=pytest.mark.skipif(_gpus() < 2, reason="RCCL data parallelism needs >= 2 GPUs")),
+    pytest.param("dp_sel_n8_32_c4.npz", "nccl",
+                 marks=pytest.mark.skipif(_gpus() < 4, reason="RCCL data parallelism needs >= 4 GPUs")),
+])
+def test_multi_rank_dp_matches_dataparallel_fixture(fname, backend, tmp_path):
     d = G.load(fname)
     world = int(d["meta_chunks"])
     port = _free_port()
@@ -37,8 +50,8 @@ def test_four_rank_dp_matches_dataparallel_fixture(tmp_path):
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
                    WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
-        procs.append(subprocess.Popen([sys.executable, "-m", "tests.dp_worker", fname, str(tmp_path)], cwd=REPO,
-                                      env=env))
+        procs.append(subprocess.Popen([sys.executable, "-m", "tests.dp_worker", fname, str(tmp_path), backend],
+                                      cwd=REPO, env=env))
     codes = []
     for p in procs:
         try:
@@ -55,7 +68,10 @@ def test_four_rank_dp_matches_dataparallel_fixture(tmp_path):
         assert len(losses) == 1, losses  # every rank computed the same global loss
         r0 = rs[0]
         res = {"loss": float(r0["loss"]), "coverage": float(r0["coverage"]),
+               "aux_loss": float(r0["aux_loss"]), "select_loss": float(r0["select_loss"]),
                "output": np.concatenate([x["output"] for x in rs]),
+               "selection": np.concatenate([x["selection"] for x in rs]),
+               "aux": np.concatenate([x["aux"] for x in rs]),
                "grads": {k[5:]: r0[k] for k in r0.files if k.startswith("grad/")},
                "params": {k[6:]: r0[k] for k in r0.files if k.startswith("param/")},
                "buffers": {k[4:]: r0[k] for k in r0.files if k.startswith("buf/")}}

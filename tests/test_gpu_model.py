@@ -21,6 +21,8 @@ from tests import _golden as G
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 PRE_BN_BIAS = {f"{n}.0.bias" for n, _, _ in L.CBR_LAYERS}
+# relative L2 gradient error against the reference's fp32 run, for fixtures without an fp64 truth
+REF32_GRAD_BOUND = 1e-3
 
 
 def build(selective, seed=0, dtype=torch.float32):
@@ -54,7 +56,8 @@ def train_step(net, opt, x, lab, selective, lamb, chunks=1):
         aux_loss = loss_A(aux, lab)
         select_loss, coverage = S.calc_selective_risk_image_b(output, sel, target=lab, lamb=lamb)
         loss = aux_loss + select_loss
-        res.update(coverage=coverage.item(), aux_loss=aux_loss.item(), select_loss=select_loss.item())
+        res.update(coverage=coverage.item(), aux_loss=aux_loss.item(), select_loss=select_loss.item(),
+                   selection=sel.detach().cpu().numpy(), aux=aux.detach().cpu().numpy())
     else:
         loss = loss_A(output, lab)
     opt.zero_grad()
@@ -75,28 +78,51 @@ def check_step(d, s, r, strict):
     assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
     if selective:
         assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
+        for k in ("aux_loss", "select_loss"):
+            assert abs(r[k] - float(d[pre + k])) <= tol * max(1.0, abs(float(d[pre + k]))), (k, r[k])
     if pre + "output" in d.files:
         assert G.max_rel(r["output"], d[pre + "output"]) < tol
     else:
         flat = r["output"].ravel()
         assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol
+    for h in ("selection", "aux"):
+        if h in r and pre + h in d.files:
+            assert G.max_rel(r[h], d[pre + h]) < tol, h
+        elif h in r and pre + h + "_idx" in d.files:
+            assert G.max_rel(r[h].ravel()[d[pre + h + "_idx"]], d[pre + h + "_val"]) < tol, h
     fails = []
     if strict:
-        mask = O.train_pred_mask(r["output"])  # train.py:150,153
-        if hashlib.sha1(mask.tobytes()).hexdigest() != d[pre + "output_mask_sha1"].item().decode():
-            assert pre + "output" in d.files, "mask hash mismatch"
-            refm = O.train_pred_mask(d[pre + "output"])
-            diff = mask != refm
-            # any flipped pixel must sit within the logit tolerance of the decision boundary
-            assert np.abs(d[pre + "output"][diff]).max() < 1e-4 * np.abs(d[pre + "output"]).max(), diff.sum()
-    if s == 0:
+        # prediction masks (train.py:150,153): report the flipped pixels; none may flip unless a
+        # reference logit lies within 1e-6 of the boundary, and any flip must sit within the
+        # logit tolerance of it
+        mask = O.train_pred_mask(r["output"])
+        same = hashlib.sha1(mask.tobytes()).hexdigest() == d[pre + "output_mask_sha1"].item().decode()
+        flips, near0 = (0, None) if same else G.mask_flips(d, pre, "output", r["output"], tol)
+        print(f"{pre}output mask: {flips} flipped pixels of {mask.size} "
+              f"(reference logits within 1e-6 of the boundary: {near0 if near0 is not None else 'n/a'})")
+        if not same and near0 == 0:
+            assert flips == 0, f"{flips} mask pixels flipped with no reference logit within 1e-6 of the boundary"
+    if s == 0 and any(k.startswith("s0/grad64norm/") for k in d.files):
         # gradients: no worse than the reference's own fp32 error against its fp64 run
         f, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
-        print("worst grad errors vs fp64 (ours, reference fp32):",
-              [(n, f"{a:.1e}", f"{b:.1e}") for n, a, b in report[:6]])
+        print("worst grad errors vs fp64 (ours, reference fp32, perturbed reference):",
+              [(n, f"{a:.1e}", f"{b:.1e}", f"{c:.1e}") for n, a, b, c in report[:6]])
         fails += f
-        fails += G.check_tensors(d, pre + "grad", r["grads"], rtol=0.0, atol=1e-6,
-                                 skip=set(r["grads"]) - PRE_BN_BIAS)  # pre-BN biases: ~0
+    elif s == 0:
+        # no fp64 run (batch 128 at 256x256 would need ~170 GB of host memory): against the
+        # reference's fp32 gradients directly (REF32_GRAD_BOUND)
+        f, report = G.check_grads_vs_ref32(d, r["grads"], REF32_GRAD_BOUND, skip=PRE_BN_BIAS)
+        print("worst grad errors vs reference fp32 (samples, norm, reference spread):",
+              [(n, f"{a:.1e}", f"{b:.1e}", f"{c:.1e}") for n, a, b, c in report[:6]])
+        fails += f
+    if s == 0:
+        # pre-BN conv biases cancel inside training-mode BN: their gradient is 0 up to rounding on
+        # both sides (fp64: ~1e-16) — ours may be no larger than the reference's own noise
+        for k in PRE_BN_BIAS & set(r["grads"]):
+            ref = d[pre + "gradfull/" + k] if pre + "gradfull/" + k in d.files else d[pre + "gradval/" + k]
+            got = np.abs(r["grads"][k]).max()
+            if got > max(1e-6, 4 * np.abs(ref).max()):
+                fails.append(f"{k}: |grad| {got:.2e} > rounding level (reference {np.abs(ref).max():.2e})")
     # (after one Adam step every element has moved by ~lr*sign(g); elements whose gradient
     # sits within rounding of zero move either way, so later-step gradients are not compared
     # element-wise — loss, logits, parameters and BN buffers are, loosely)
@@ -217,9 +243,9 @@ def test_adam_matches_reference_algorithm():
 def test_step_against_oracle_shapes(input_type, n, h, w, selective):
     """One fp32 training step (forward, losses, backward) against the CPU oracle at shapes the
     fixtures do not cover. Loss within 1e-4 relative of the oracle's fp32 run; gradients judged
-    as in check_step: relative-L2 error against the oracle's fp64 run no worse than
-    max(3 x the oracle fp32 run's own error, 1e-2) (ReLU / max-pool near-ties route
-    fp32 gradients differently under any change of summation order)."""
+    as in check_step: relative-L2 error against the oracle's fp64 run within tests/_golden.grad_bound
+    of the oracle fp32 run's own error (ReLU / max-pool near-ties route fp32
+    gradients differently under any change of summation order)."""
     x, lab = make_batch(n, max(h, w), seed=11)
     x = np.ascontiguousarray(x[:, :L.input_channels(input_type), :h, :w])
     lab = np.ascontiguousarray(lab[:, :h, :w])
@@ -240,11 +266,11 @@ def test_step_against_oracle_shapes(input_type, n, h, w, selective):
     loss.backward()
     torch.cuda.synchronize()
 
-    def oracle(dt):
+    def oracle(dt, xin=x):
         params, buffers = O.make_state(3, input_type, selective)
         params = {k: v.detach().to(dt).requires_grad_() for k, v in params.items()}
         buffers = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in buffers.items()}
-        xo, lo = torch.tensor(x, dtype=dt), torch.tensor(lab, dtype=dt)
+        xo, lo = torch.tensor(xin, dtype=dt), torch.tensor(lab, dtype=dt)
         ro = O.forward(params, buffers, xo, selective, training=True)
         if selective:
             o2, s2, a2 = ro
@@ -258,10 +284,20 @@ def test_step_against_oracle_shapes(input_type, n, h, w, selective):
     loss32, g32 = oracle(torch.float32)
     _, g64 = oracle(torch.float64)
     assert abs(loss.item() - loss32) < 1e-4 * max(1.0, abs(loss32))
+    # the oracle's own fp32 error on 4 rounding-level perturbations of the input (the e_ens of
+    # tests/_golden.grad_bound)
+    ens = {}
+    for m in range(1, 5):
+        rng = np.random.Generator(np.random.PCG64(1000 + m))
+        xp = (x.astype(np.float64) * (1.0 + 1e-7 * rng.standard_normal(x.shape))).astype(np.float32)
+        _, p32 = oracle(torch.float32, xp)
+        _, p64 = oracle(torch.float64, xp)
+        for k in p64:
+            ens[k] = max(ens.get(k, 0.0), float((p32[k] - p64[k]).norm() / (p64[k].norm() + 1e-30)))
     for k, q in net.named_parameters():
         if k in PRE_BN_BIAS:  # cancels inside training-mode BN: zero gradient on both sides
             continue
         nrm = float(g64[k].norm()) + 1e-30
         err = float((q.grad.cpu().double() - g64[k]).norm()) / nrm
         err_ref = float((g32[k] - g64[k]).norm()) / nrm
-        assert err <= max(3 * err_ref, 1e-2), (k, err, err_ref)
+        assert err <= G.grad_bound(err_ref, ens[k]), (k, err, err_ref, ens[k])

@@ -119,3 +119,41 @@ def test_argmax_rule_threshold_is_strict_positive():
     assert t > 0 and np.nextafter(np.float32(0), np.float32(1)) == t
     for d in (np.float32(0), np.float32(-0.0), np.float32(1e-45), np.float32(-1e-45), np.float32(3.0)):
         assert bool(d >= t) == bool(d > 0)
+
+
+def test_spawn_stops_all_ranks_when_any_rank_fails():
+    """train.spawn polls every child: a failing rank 1 ends the job at once (rank 0, still
+    running, is terminated) instead of after rank 0's own exit."""
+    import sys
+    import time
+
+    from selectivenet_for_semantic_segmentation_binary_amd.train import spawn
+
+    child = ("import os, sys, time\n"
+             "r = int(os.environ['RANK'])\n"
+             "sys.exit(3) if r == 1 else time.sleep(60)\n")
+    t0 = time.perf_counter()
+    rc = spawn([], [0, 1, 2], command=[sys.executable, "-c", child])
+    assert rc != 0
+    assert time.perf_counter() - t0 < 30
+
+
+def test_decode_patch_list_cache_is_written_atomically(tmp_path):
+    """The uint8 cache is written under a temporary name and renamed into place: after a decode
+    only the finished .npy files remain, and a second call memory-maps them."""
+    from PIL import Image
+
+    root = tmp_path / "200x_16"
+    root.mkdir()
+    rng = np.random.default_rng(0)
+    pairs = []
+    for i in range(3):
+        Image.fromarray(rng.integers(0, 255, (16, 16, 3), dtype=np.uint8)).save(root / f"p{i}_input.png")
+        Image.fromarray((rng.random((16, 16)) > 0.5).astype(np.uint8) * 255).save(root / f"p{i}_label.png")
+        pairs.append((f"p{i}_input.png", f"p{i}_label.png"))
+    a = D.decode_patch_list(str(tmp_path), pairs, 200, 16)
+    files = sorted(os.listdir(root / "_selunet_cache"))
+    assert len(files) == 2 and all(f.endswith(".npy") and ".tmp" not in f for f in files)
+    b = D.decode_patch_list(str(tmp_path), pairs, 200, 16)
+    assert isinstance(b.images, np.memmap) and np.array_equal(np.asarray(b.images), a.images)
+    assert np.array_equal(np.asarray(b.labels), a.labels)

@@ -1,6 +1,7 @@
-"""Per-layer timing of the 3x3 conv kernels at the bench shapes (bs=128, bf16) — profiling tool.
+"""Per-layer timing of the 3x3 conv kernels at the bench shapes (bs=128) — profiling tool.
 
     python tools/conv_bench.py [--batch 128] [--iters 20] [--only fwd|dgrad|wgrad] [--layers enc1_2,dec1_2]
+                               [--dtype bf16|fp32]
 
 Calls selunet_gemm_gather directly on random NHWC operands (forward: BN+ReLU transform of the
 producer applied on load, BN-stat epilogue; dgrad: untransformed dY, the SPLIT epilogue where the
@@ -120,25 +121,27 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--layers", default="")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     sel = set(a.layers.split(",")) if a.layers else None
     tot_ms, tot_fl = 0.0, 0.0
     for name, (c0, c1), co, hw in LAYERS:
         if sel and name not in sel:
             continue
         if a.only not in ("dgrad", "wgrad"):
-            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters)
+            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
         if a.only == "wgrad":
-            ms, tf, kn = run_wgrad(a.batch, (c0, c1), co, hw, a.iters)
+            ms, tf, kn = run_wgrad(a.batch, (c0, c1), co, hw, a.iters, dt)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
             continue
         if a.only != "fwd":
-            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters)
+            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"dgrad {name:8s} {co:4d}->{c0 + c1:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
