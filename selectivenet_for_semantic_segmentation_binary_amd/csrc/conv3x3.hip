@@ -798,42 +798,54 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
 }
 
 // fp32 weight gradient (v_mfma_f32_32x32x2_f32: exact fp32 products, the parity configuration).
-// Same wave roles as the bf16 kernel on an 8 x 8-pixel tile (10 x 10 halo: the register-held
-// prefetch of the next tile then fits beside the 9 tap accumulators without spilling); an MFMA operand is one fp32 per lane
-// (A[i = co][k = pixel], B[k = pixel][j = ci]), read with ds_read_b32 straight from the natural
-// [pixel][channel] tiles: lanes 0-31 take pixel 2s and lanes 32-63 pixel 2s + 1, the two 32-lane
-// groups of ds_read_b32 never conflict with each other and 32 consecutive floats in a group hit 32
-// distinct banks, so the tiles need no padding or swizzle. One dY fragment feeds the MFMAs of all
-// the wave's taps (9, or 5/4 when BI = 64). At the fp32 MFMA rate a pixel tile keeps every SIMD
-// busy for ~70k cycles, so one LDS buffer is enough: the next tile's loads are in registers during
-// the current tile's MFMAs and are written (BN+ReLU applied, padding zeroed) between two barriers.
-// (A 16-pixel-wide tile would need 56 prefetch registers per lane and spills at 2 waves per SIMD.)
+// An MFMA operand is one fp32 per lane (A[i = co][k = pixel], B[k = pixel][j = ci]), read with
+// ds_read_b32 straight from the natural [pixel][channel] tiles: lanes 0-31 take pixel 2s and
+// lanes 32-63 pixel 2s + 1 — the two 32-lane groups of ds_read_b32 never conflict with each other
+// and 32 consecutive floats in a group hit 32 distinct banks, so the tiles need no padding.
+//
+// 512 threads (two waves per SIMD). A wave owns WCO co x 32 ci and one group of taps: BI = 128
+// with WCO = 64 splits the 9 taps in two groups (5 / 4), BI = 64 with WCO = 32 likewise, so a
+// wave keeps at most 10 accumulators and per k-step issues WCO/32 dY reads + one halo read per
+// tap for (WCO/32) x taps MFMAs; the operands of the next k-step are read while the current one
+// multiplies. The pixel tile is 8 x 8 (10 x 10 halo) and LDS holds two tiles: the next tile's
+// loads are issued before a tile's MFMAs and written (BN+ReLU of the producer applied, padding
+// zeroed) into the other buffer after them, so a tile boundary costs one barrier. Measured against
+// the alternatives (tools/ab_wgrad.sh, fp32 bs=128 layers): 9 taps per wave at 2 waves/SIMD
+// 118 TF/s; one wave per SIMD with 18 accumulators 85; the next tile written to LDS in the middle
+// of the MFMA loop 98-107; this layout 126 (BI = 128) / 118 (BI = 64).
 constexpr int FTH = 8, FTW = 8;                  // fp32 pixel tile
 
-template <int BI>
+template <int BI, int WCO>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int co_tiles,
                               int ci_chunks, int64_t tiles_per_split, int tiles_x, int tiles_y, int64_t total_tiles,
                               float* __restrict__ ws, int64_t ws_stride) {
   constexpr int CJ = 64;                         // ci channels per chunk
   constexpr int WTH = FTH, WTW = FTW, WHW = FTW + 2, WPIXT = FTH * FTW, WHP = (FTH + 2) * (FTW + 2);
-  constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
-  constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
-  constexpr int P_ROUNDS = (WPIXT * BI / 4) / 512;
-  constexpr int X_ROUNDS = (WHP * (CJ / 4) + 511) / 512;
-  static_assert(P_ROUNDS * 512 == WPIXT * BI / 4, "dY tile must split evenly over the threads");
+  constexpr int NT = 512;
+  constexpr int MA = WCO / 32;                   // co subtiles per wave
+  constexpr int COH = BI / WCO;                  // co groups
+  constexpr int TGN = 8 / (COH * 2);             // tap groups: 2 (taps 0-4, 5-8) or 4 (0-2, 3-4, 5-6, 7-8)
+  static_assert(TGN == 2 || TGN == 4, "8 waves = co groups x 2 ci halves x tap groups");
+  constexpr int NTAP = TGN == 2 ? 5 : 3;
+  constexpr int P_ROUNDS = (WPIXT * BI / 4) / NT;
+  constexpr int X_ROUNDS = (WHP * (CJ / 4) + NT - 1) / NT;
+  constexpr int KS = WPIXT / 2;                  // k-steps per tile
+  // k-steps unrolled: 4 at BI = 64 (120 vs 110 TF/s), 2 at BI = 128 (4 spills 22 registers: 126 vs 119)
+  constexpr int UNR = BI == 128 ? 2 : 4;
+  static_assert(P_ROUNDS * NT == WPIXT * BI / 4, "dY tile must split evenly over the threads");
 
-  __shared__ __attribute__((aligned(16))) float Ps[WPIXT][BI];
-  __shared__ __attribute__((aligned(16))) float Xs[WHP][CJ];
+  __shared__ __attribute__((aligned(16))) float Ps[2][WPIXT][BI];
+  __shared__ __attribute__((aligned(16))) float Xs[2][WHP][CJ];
   __shared__ float Ks[2 * BI + 2 * CJ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wj = wave & 1;
-  const int wi = (wave >> 1) % (BI / 32);
-  const int tg = (wave >> 1) / (BI / 32);
-  const int tap0 = tg * 5;
-  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
+  const int wj = wave & 1;                       // ci half (32 channels)
+  const int wc = (wave >> 1) % COH;              // co group
+  const int tg = (wave >> 1) / COH;              // tap group
+  const int tap0 = TGN == 2 ? tg * 5 : (tg == 0 ? 0 : 1 + 2 * tg);
+  const int ntap = TGN == 2 ? (tg == 0 ? 5 : 4) : (tg == 0 ? 3 : 2);
   const int half = lane >> 5, l32 = lane & 31;
 
   const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -883,117 +895,137 @@ conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out,
     }
     return v;
   };
+  // raw loads of a tile's dY part / halo part (pixels clamped into the image; zeroed when written)
   f32x4 rp[P_ROUNDS], rx[X_ROUNDS];
-  auto load_tile = [&](int pt) __attribute__((always_inline)) {
+  auto load_p = [&](int pt) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
+      const int idx = r * NT + tid;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const int y = min(y0 + px / WTW, H - 1), x = min(x0 + px % WTW, W - 1);
       rp[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pa.data) +
                                               (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4);
     }
+  };
+  auto load_x = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < X_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
+      const int idx = r * NT + tid;
       const int hp = min(idx >> 4, WHP - 1), cc = idx & 15;
       const int y = min(max(y0 - 1 + hp / WHW, 0), H - 1), x = min(max(x0 - 1 + hp % WHW, 0), W - 1);
       rx[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(xa.data) +
                                               (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 4);
     }
   };
-  auto store_tile = [&](int pt) __attribute__((always_inline)) {
+  auto store_p = [&](int pt, int buf) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
+      const int idx = r * NT + tid;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
       if (y0 + px / WTW < H && x0 + px % WTW < W)
         v = pa.scale ? apply(rp[r], Ks + cc * 4, Ks + BI + cc * 4, pa.relu) : rp[r];
-      *reinterpret_cast<f32x4*>(&Ps[px][cc * 4]) = v;
+      *reinterpret_cast<f32x4*>(&Ps[buf][px][cc * 4]) = v;
     }
+  };
+  auto store_x = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < X_ROUNDS; ++r) {
-      const int idx = r * 512 + tid;
+      const int idx = r * NT + tid;
       if (idx < WHP * (CJ / 4)) {
         const int hp = idx >> 4, cc = idx & 15;
         const int y = y0 - 1 + hp / WHW, x = x0 - 1 + hp % WHW;
         f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
         if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
           v = xa.scale ? apply(rx[r], Ks + 2 * BI + cc * 4, Ks + 2 * BI + CJ + cc * 4, xa.relu) : rx[r];
-        *reinterpret_cast<f32x4*>(&Xs[hp][cc * 4]) = v;
+        *reinterpret_cast<f32x4*>(&Xs[buf][hp][cc * 4]) = v;
       }
     }
   };
 
-  f32x16 acc[NTAP];
+  f32x16 acc[MA][NTAP];
 #pragma unroll
-  for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
+  for (int a = 0; a < MA; ++a)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) acc[a][t] = f32x16{};
 
-  // per-lane LDS element offsets: dY column, halo column and each tap's halo pixel offset
-  const float* pcol = &Ps[0][wi * 32 + l32];
-  const float* xcol = &Xs[0][wj * 32 + l32];
   int toff[NTAP];
 #pragma unroll
   for (int t = 0; t < NTAP; ++t) {
     const int tap = min(tap0 + t, 8);
     toff[t] = ((tap / 3) * WHW + tap % 3) * CJ;
   }
+  struct Frag {
+    float a[MA], b[NTAP];
+  };
+  // operands of k-step ks (k = the lane half's pixel) from buffer buf
+  auto frag = [&](int buf, int ks) __attribute__((always_inline)) {
+    Frag f;
+    const int p = 2 * ks + half;
+    const float* pr = &Ps[buf][p][wc * WCO + l32];
+#pragma unroll
+    for (int a = 0; a < MA; ++a) f.a[a] = pr[a * 32];
+    const float* xr = &Xs[buf][(p / WTW) * WHW + p % WTW][wj * 32 + l32];
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) f.b[t] = xr[toff[t]];
+    return f;
+  };
 
-  load_tile((int)pt_begin);
+  load_p((int)pt_begin);
+  load_x((int)pt_begin);
   __syncthreads();  // coefficients visible
-  store_tile((int)pt_begin);
+  store_p((int)pt_begin, 0);
+  store_x((int)pt_begin, 0);
   __syncthreads();
+  int buf = 0;
   for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
     const bool more = pt + 1 < (int)pt_end;
-    load_tile(more ? pt + 1 : pt);
-    __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
-    // operands of k-step ks + 1 are read while k-step ks multiplies (the last step re-reads step 0:
-    // valid addresses, unused)
-    struct Frag {
-      float a, b[NTAP];
-    };
-    auto frag = [&](int ks) __attribute__((always_inline)) {
-      Frag f;
-      const int p = 2 * ks + half;                        // k = pixel of this lane's half
-      f.a = pcol[p * BI];
-      const int hbase = ((p / WTW) * WHW + p % WTW) * CJ;  // halo pixel of tap (0, 0)
-#pragma unroll
-      for (int t = 0; t < NTAP; ++t) f.b[t] = xcol[hbase + toff[t]];
-      return f;
-    };
-    Frag cur = frag(0);
-#pragma unroll 2
-    for (int ks = 0; ks < WPIXT / 2; ++ks) {
-      const Frag nxt = frag(ks + 1 < WPIXT / 2 ? ks + 1 : 0);
+    if (more) { load_p(pt + 1); load_x(pt + 1); }
+    Frag cur = frag(buf, 0);
+#pragma unroll UNR
+    for (int ks = 0; ks < KS; ++ks) {
+      const Frag nxt = frag(buf, ks + 1 < KS ? ks + 1 : 0);
 #pragma unroll
       for (int t = 0; t < NTAP; ++t)
-        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a, cur.b[t], acc[t], 0, 0, 0);
+        if (t < ntap) {
+#pragma unroll
+          for (int a = 0; a < MA; ++a)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[a], cur.b[t], acc[a][t], 0, 0, 0);
+        }
+
       cur = nxt;
     }
-    __syncthreads();  // every wave is done reading the tile
-    if (more) {
-      store_tile(pt + 1);
-      __syncthreads();
-    }
+    if (more) { store_p(pt + 1, buf ^ 1); store_x(pt + 1, buf ^ 1); }
+    __syncthreads();  // the next tile is in buf ^ 1; everyone is done with buf
+    buf ^= 1;
   }
 
+  // (an opaque copy of the lane: the store addresses below are loop-invariant, and hoisting them
+  // above the tile loop would pin ~70 registers through it)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
   const int ctot = Q.Ctot;
 #pragma unroll
   for (int t = 0; t < NTAP; ++t) {
     if (t < ntap) {
       const int tap = tap0 + t;
-      const int j = tap * ctot + c0 + wj * 32 + l32;
+      const int j = tap * ctot + c0 + wj * 32 + (ln & 31);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[t][r];
-        else atomicAdd(out + (int64_t)i * ldo + j, acc[t][r]);
-      }
+      for (int a = 0; a < MA; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = i0 + wc * WCO + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+          if (ws) ws[split * ws_stride + (int64_t)i * ldo + j] = acc[a][t][r];
+          else atomicAdd(out + (int64_t)i * ldo + j, acc[a][t][r]);
+        }
     }
   }
 }
@@ -1051,11 +1083,11 @@ int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out
   const int64_t stride = (int64_t)ni * ldo;
   if (dtype == SELUNET_F32) {
     if (bi == 128)
-      hipLaunchKernelGGL(conv3x3_wgrad_halo_f32_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
-                         ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
+      hipLaunchKernelGGL((conv3x3_wgrad_halo_f32_kernel<128, 64>), dim3(blocks), dim3(512), 0, st, p, q, out, ldo,
+                         co_tiles, ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
     else
-      hipLaunchKernelGGL(conv3x3_wgrad_halo_f32_kernel<64>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
-                         ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
+      hipLaunchKernelGGL((conv3x3_wgrad_halo_f32_kernel<64, 32>), dim3(blocks), dim3(512), 0, st, p, q, out, ldo,
+                         co_tiles, ci_chunks, per, tiles_x, tiles_y, total, ws, stride);
   } else if (bi == 128)
     hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<128>, dim3(blocks), dim3(512), 0, st, p, q, out, ldo, co_tiles,
                        ci_chunks, per, tiles_x, tiles_y, total, ws, stride);

@@ -26,6 +26,8 @@ NAME_MAP = [
     (r"conv3x3_halo_kernelIDF16bLi64", "conv3x3_halo<bf16,64>"),
     (r"conv3x3_halo_kernelIfLi128", "conv3x3_halo<f32,128>"),
     (r"conv3x3_halo_kernelIfLi64", "conv3x3_halo<f32,64>"),
+    (r"conv3x3_wgrad_halo_f32_kernelILi128", "conv3x3_wgrad_halo_f32<128>"),
+    (r"conv3x3_wgrad_halo_f32_kernelILi64", "conv3x3_wgrad_halo_f32<64>"),
     (r"conv3x3_wgrad_halo_kernel<128>|conv3x3_wgrad_halo_kernelILi128", "conv3x3_wgrad_halo<128>"),
     (r"conv3x3_wgrad_halo_kernel<64>|conv3x3_wgrad_halo_kernelILi64", "conv3x3_wgrad_halo<64>"),
     (r"gemm_gather_kernelIDF16b", "gemm_gather<bf16>"),

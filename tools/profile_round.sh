@@ -10,7 +10,7 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
-B="python3 $root/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-kernel-timing"
+B="python3 $root/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-kernel-timing --no-full-loop ${BENCH_ARGS:-}"
 run() {  # name seconds rocprof-args...
   local name=$1 secs=$2; shift 2
   echo "== $name" >&2
