@@ -228,6 +228,20 @@ int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, doubl
                               float* running_mean, float* running_var, int64_t* num_batches,
                               float momentum, float eps, float* mean, float* invstd, float* scale,
                               float* shift, void* stream);
+/* Second (centered) pass of the batch statistics, fp32 parity configuration: slab [rows][2][c] of
+ * per-channel sums of (y - center) and (y - center)^2 over y [m][c] (center = the first pass's
+ * batch mean; rows = selunet_channel_slab_rows(m)); then selunet_bn_stats_finalize_centered
+ * reduces it like selunet_bn_stats_finalize (mean = center + E[y - center], var = E[(y - center)^2]
+ * - E[y - center]^2) and writes the same outputs — `mean` may alias `center`. Same role as
+ * selunet_bn_stats_finalize (model.py:12 BatchNorm2d batch statistics), numerically two-pass. */
+int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab,
+                                 int32_t dtype, void* stream);
+int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums,
+                                       int64_t count, int32_t c, const float* center,
+                                       const float* conv_bias, const float* gamma, const float* beta,
+                                       float* running_mean, float* running_var, int64_t* num_batches,
+                                       float momentum, float eps, float* mean, float* invstd,
+                                       float* scale, float* shift, void* stream);
 int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums,
                                   int64_t count, int32_t c, const float* gamma, const float* invstd,
                                   float* dgamma, float* dbeta, float* dbias, float* coef,

@@ -99,6 +99,9 @@ SIGNATURES = {
     "selunet_pack_weights": (c_int32, [ctypes.POINTER(PackList), c_int32, P]),
     "selunet_bn_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, c_float, c_float,
                                             P, P, P, P, P]),
+    "selunet_bn_centered_partials": (c_int32, [P, c_int64, c_int32, P, P, c_int32, P]),
+    "selunet_bn_stats_finalize_centered": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P,
+                                                     c_float, c_float, P, P, P, P, P]),
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),

@@ -475,7 +475,9 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   rb_next = b_load(1 % csteps);
   __syncthreads();
 
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  using Acc = typename StatAcc<T>::type;
+  static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
+  Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const TileStats ts = tile_stats(ep, prow, n0, N);
   float* tile = reinterpret_cast<float*>(smem);  // epilogue: [256][BN + 4] over the whole LDS
   uint4 ra[A_ROUNDS];

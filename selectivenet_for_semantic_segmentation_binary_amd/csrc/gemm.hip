@@ -205,7 +205,9 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   int64_t* rowbase = reinterpret_cast<int64_t*>(smem + BM * (BN + 4) * 4);
   const int Cq = N >> 2;
   const TileStats ts = tile_stats(ep, prow, n0, N);
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  using Acc = typename StatAcc<T>::type;
+  static_assert(stats_flush_bytes<BN, 256, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
+  Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto epilogue = [&](const f32x16 (&acc)[MT][NT], int64_t m_tile) __attribute__((always_inline)) {
     const int64_t m0 = m_tile * BM;
     acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);

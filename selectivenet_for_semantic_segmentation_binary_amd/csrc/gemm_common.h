@@ -237,16 +237,26 @@ __device__ __forceinline__ TileStats tile_stats(const EpiArg& ep, int64_t row, i
   return ts;
 }
 
+// Accumulator type of the per-thread statistics a persistent workgroup carries across its tiles:
+// double for fp32 operands — a workgroup folds hundreds of values per column into each thread's
+// sums, and these sums (BN batch mean / E[y^2], the BN-backward sum of dA that becomes the bias
+// gradient, ConvTranspose2d bias sums) are cancellation-prone: fp32 sequential accumulation put a
+// 512x512 bias gradient 2.5e-3 off the reference where the reference's own spread is 1.5e-4 —
+// and float for bf16 operands, whose rounding dominates anyway.
+template <typename T> struct StatAcc { using type = float; };
+template <> struct StatAcc<float> { using type = double; };
+
 // Store the LDS tile as 8-column vectors (16 B bf16 / 32 B fp32): dst(row, col) returns the
 // global address of tile element (row, col) (col a multiple of 8) or nullptr for a masked row.
 // bias (nullable) is indexed by bias_col(col).
-// The statistics are accumulated into the thread's s1/s2/s3 (8 columns each: the thread's column
-// chunk is tid % (TC / 8) for every tile, so a persistent workgroup can accumulate over its tiles)
-// and reduced across the workgroup by tile_stats_flush.
-template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>
+// The statistics of this tile are summed per thread in fp32 (a few rows) and added into the
+// thread's s1/s2/s3 (8 columns each: the thread's column chunk is tid % (TC / 8) for every tile,
+// so a persistent workgroup can accumulate over its tiles, in Acc precision) and reduced across the
+// workgroup by tile_stats_flush.
+template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol, typename Acc>
 __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& dst, const float* bias,
-                                                   BiasCol&& bias_col, const TileStats& ts, float (&s1)[8],
-                                                   float (&s2)[8], float (&s3)[8]) {
+                                                   BiasCol&& bias_col, const TileStats& ts, Acc (&s1)[8],
+                                                   Acc (&s2)[8], Acc (&s3)[8]) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass
   // an opaque copy of tid: in a persistent kernel the column coefficients below are invariant over
@@ -270,6 +280,7 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       is[e] = ts.bnb.invstd[col + e];
     }
   }
+  float t1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
@@ -279,8 +290,8 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
     if (do_st) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        s1[e] += v[e];
-        s2[e] += v[e] * v[e];
+        t1[e] += v[e];
+        t2[e] += v[e] * v[e];
       }
     }
 #pragma unroll
@@ -298,7 +309,7 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
     }
     if (do_cs) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s1[e] += to_f(o[e]);
+      for (int e = 0; e < 8; ++e) t1[e] += to_f(o[e]);
     }
     if (do_bn) {
       const T* yp = reinterpret_cast<const T*>(ts.bnb.y) + (p - reinterpret_cast<const T*>(ts.out0));
@@ -316,21 +327,33 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
         const float y = to_f(yv[e]);
         const float da = y * sc[e] + sh[e] > 0.0f ? to_f(o[e]) : 0.0f;
         const float xh = (y - mu[e]) * is[e];
-        s1[e] += da;
-        s2[e] += da * xh;
-        s3[e] += xh;
+        t1[e] += da;
+        t2[e] += da * xh;
+        t3[e] += xh;
       }
     }
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] += (Acc)t1[e];
+    s2[e] += (Acc)t2[e];
+    s3[e] += (Acc)t3[e];
+  }
 }
 
+// LDS bytes tile_stats_flush needs for accumulators of type Acc
+template <int TC, int NTHREADS, typename Acc>
+constexpr int stats_flush_bytes() { return (NTHREADS / (TC / 8)) * TC * 3 * (int)sizeof(Acc); }
+
 // Reduce the s1/s2/s3 accumulators of lds_tile_store_acc over the workgroup (LDS scratch `red`,
-// RS * TC * 3 floats; the caller has finished with whatever `red` held) and write the slab row.
-template <int TC, int NTHREADS>
-__device__ __forceinline__ void tile_stats_flush(float* red, int tid, const TileStats& ts, const float (&s1)[8],
-                                                 const float (&s2)[8], const float (&s3)[8]) {
+// stats_flush_bytes bytes; the caller has finished with whatever `red` held) and write the slab
+// row (fp32).
+template <int TC, int NTHREADS, typename Acc>
+__device__ __forceinline__ void tile_stats_flush(float* red_f, int tid, const TileStats& ts, const Acc (&s1)[8],
+                                                 const Acc (&s2)[8], const Acc (&s3)[8]) {
   constexpr int CC = TC / 8;
   constexpr int RS = NTHREADS / CC;
+  Acc* red = reinterpret_cast<Acc*>(red_f);
   const int cc = tid % CC, r0 = tid / CC;
   const int col = cc * 8;
   const bool do_st = ts.stats != nullptr;
@@ -347,7 +370,7 @@ __device__ __forceinline__ void tile_stats_flush(float* red, int tid, const Tile
     __syncthreads();
     for (int i = tid; i < TC * nst; i += NTHREADS) {
       const int c = i % TC, k = i / TC;
-      float a = 0.0f;
+      Acc a = 0;
       for (int r = 0; r < RS; ++r) a += red[(r * TC + c) * 3 + k];
       if (do_bn) ts.bnb.slab[k * ts.ld + c] = a;
       else if (do_st) ts.stats[k * ts.ld + c] = a;

@@ -185,7 +185,10 @@ __global__ void reduce_rows_l2(const double* __restrict__ ws, int splits, int co
   }
 }
 
-int64_t channel_slab_rows(int64_t m) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(m, 256), 2048)); }
+// up to 8192 blocks: at 8.4M pixels a pixel lane then folds 64 values (C = 64) sequentially in fp32
+// before the fixed-order fp64 reduction of the slab (2048 blocks: 256 — the per-channel sums
+// here, e.g. the BN-backward sum of dA, cancel, so long fp32 runs cost digits)
+int64_t channel_slab_rows(int64_t m) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(m, 256), 8192)); }
 
 // Per-channel reduction skeleton over an NHWC [m][C] range: PL pixel lanes x (C/4) channel groups.
 // C in {64,128,256,512}.
@@ -228,6 +231,24 @@ __global__ void channel_sum_kernel(const T* __restrict__ x, int64_t m, int C, fl
   channel_block_reduce<1>(acc, C, slab + (int64_t)blockIdx.x * C);
 }
 
+// Second pass of the BatchNorm batch statistics: per-channel sums of d = y - center and d^2
+// (center = the first pass's mean) -> slab [rows][2][C]. E[y^2] - mean^2 from the conv epilogue's
+// sums loses ~eps * mean^2 / var of the variance (the first layer's invstd came out 14x further from
+// the fp64 value than the reference's); the centered sums do not.
+template <typename T>
+__global__ void bn_centered_partials_kernel(const T* __restrict__ y, int64_t m, int C, const float* __restrict__ center,
+                                            float* slab) {
+  f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  const int c0 = (threadIdx.x % (C >> 2)) * 4;
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(center + c0);
+  channel_loop<T>(m, C, [&](int64_t p, int c) {
+    const f32x4 d = Vec4<T>::load(y + p * C + c) - mu;
+    acc[0] += d;
+    acc[1] += d * d;
+  });
+  channel_block_reduce<2>(acc, C, slab + (int64_t)blockIdx.x * 2 * C);
+}
+
 // =========================================================================== BatchNorm
 // one channel of the BatchNorm finalize: batch statistics from the fp64 sums (training) or the
 // running statistics (eval) -> mean (of the conv output without bias), invstd, folded scale/shift
@@ -242,14 +263,16 @@ struct BnFinArgs {
   float momentum, eps;
   int training;
   float *mean_o, *invstd_o, *scale_o, *shift_o;
+  const float* center;  // non-NULL: s_sum / s_sq are sums of (y - center) and (y - center)^2
 };
 
 __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const BnFinArgs& a) {
   const double b = a.conv_bias ? (double)a.conv_bias[c] : 0.0;
   double mean, var;
   if (a.training) {
-    mean = s_sum / (double)a.count;
-    var = s_sq / (double)a.count - mean * mean;
+    const double d = s_sum / (double)a.count;  // mean of y - center
+    mean = (a.center ? (double)a.center[c] : 0.0) + d;
+    var = s_sq / (double)a.count - d * d;      // centered: no cancellation against mean^2
     if (var < 0) var = 0;
     if (a.rmean) a.rmean[c] = (float)((1.0 - a.momentum) * a.rmean[c] + a.momentum * (mean + b));
     if (a.rvar)
@@ -1230,6 +1253,28 @@ int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, doubl
                      mean, invstd, scale, shift};
   launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
   return check_launch("bn_stats_finalize");
+}
+
+int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab, int32_t dtype,
+                                 void* stream) {
+  SELUNET_REQUIRE(y && center && slab && m > 0 && ok_channels(c), "bn_centered_partials: bad arguments (C=%d)", c);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB),
+                                       0, as_stream(stream), (const T*)y, m, c, center, slab));
+  return check_launch("bn_centered_partials");
+}
+
+int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,
+                                       int32_t c, const float* center, const float* conv_bias, const float* gamma,
+                                       const float* beta, float* running_mean, float* running_var,
+                                       int64_t* num_batches, float momentum, float eps, float* mean, float* invstd,
+                                       float* scale, float* shift, void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && center && gamma && beta && mean && invstd && scale && shift && c > 0,
+                  "bn_stats_finalize_centered: bad arguments");
+  SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
+  const BnFinArgs fa{count, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, 1,
+                     mean, invstd, scale, shift, center};
+  launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
+  return check_launch("bn_stats_finalize_centered");
 }
 
 int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,

@@ -207,7 +207,24 @@ class Engine:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
             K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
         mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
-        if ctx.training:  # statistics slab -> fp64 column sums -> batch mean/invstd, running stats: one launch
+        if ctx.training and self.dt == torch.float32:
+            # fp32 (parity): two-pass statistics — the epilogue's sums give the batch mean, a second
+            # pass over y sums (y - mean) and (y - mean)^2 for the variance, then the finalize with the
+            # running-statistic updates (selunet_bn_centered_partials)
+            ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
+            K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
+                   K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+                   None, None, None, BN_MOMENTUM, BN_EPS, K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift),
+                   self.stream)
+            rows2 = K.query("selunet_channel_slab_rows", M)
+            slab2 = K.keep(torch.empty(rows2, 2, co, dtype=torch.float32, device=dev))
+            K.call("selunet_bn_centered_partials", K.ptr(y), M, co, K.ptr(mean), K.ptr(slab2), self.code, self.stream)
+            K.call("selunet_bn_stats_finalize_centered", K.ptr(slab2), rows2, K.ptr(ws), None, M, co, K.ptr(mean),
+                   K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+                   K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
+                   K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS,
+                   K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+        elif ctx.training:  # statistics slab -> fp64 column sums -> batch mean/invstd, running stats: one launch
             ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
             K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
                    K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
