@@ -1,6 +1,8 @@
 // Device-side operand descriptors and helpers shared by the implicit-GEMM kernels.
 #pragma once
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace selunet {
@@ -280,7 +282,12 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       is[e] = ts.bnb.invstd[col + e];
     }
   }
-  float t1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // per-tile fp32 partials; with fp32 accumulators they are the accumulators themselves
+  constexpr bool WIDE = !std::is_same<Acc, float>::value;
+  float tw1[WIDE ? 8 : 1] = {}, tw2[WIDE ? 8 : 1] = {}, tw3[WIDE ? 8 : 1] = {};
+  float* t1 = WIDE ? tw1 : reinterpret_cast<float*>(s1);
+  float* t2 = WIDE ? tw2 : reinterpret_cast<float*>(s2);
+  float* t3 = WIDE ? tw3 : reinterpret_cast<float*>(s3);
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
@@ -333,11 +340,13 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       }
     }
   }
+  if constexpr (WIDE) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    s1[e] += (Acc)t1[e];
-    s2[e] += (Acc)t2[e];
-    s3[e] += (Acc)t3[e];
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += (Acc)t1[e];
+      s2[e] += (Acc)t2[e];
+      s3[e] += (Acc)t3[e];
+    }
   }
 }
 
