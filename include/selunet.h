@@ -257,6 +257,18 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
 int selunet_memset(void* dst, int32_t value, int64_t bytes, void* stream);
 int selunet_memcpy(void* dst, const void* src, int64_t bytes, void* stream);
 
+/* ---- HIP graphs of recorded launch plans ---------------------------------------------------
+ * A replayed launch plan (a whole forward or backward pass, ~100 launches) is captured once into
+ * a hipGraph and afterwards issued with one selunet_graph_launch instead of one host call per
+ * kernel. Capture runs on a private non-blocking stream (the default stream cannot capture);
+ * the instantiated graph is then launched on the caller's stream. */
+int selunet_stream_create(void** out);
+int selunet_stream_destroy(void* stream);
+int selunet_graph_capture_begin(void* stream);
+int selunet_graph_capture_end(void* stream, void** exec);
+int selunet_graph_launch(void* exec, void* stream);
+int selunet_graph_destroy(void* exec);
+
 /* ---- first layer (C_in = 3 or 2, model.py:24-29) --------------------------------------- */
 /* x NCHW fp32 -> out [n*h*w][k_pad] in dtype: column tap*c + ci of the 3x3 pad-1 window, zero
  * for columns >= 9c. The first conv then runs as selunet_gemm_gather with taps = 1. */

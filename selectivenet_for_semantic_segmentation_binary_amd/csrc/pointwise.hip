@@ -1202,6 +1202,54 @@ int selunet_memcpy(void* dst, const void* src, int64_t bytes, void* stream) {
   return 0;
 }
 
+int selunet_stream_create(void** out) {
+  SELUNET_REQUIRE(out, "stream_create: bad arguments");
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipStreamCreateWithFlags failed");
+  *out = s;
+  return 0;
+}
+
+int selunet_stream_destroy(void* s) {
+  if (s && hipStreamDestroy(as_stream(s)) != hipSuccess) return fail(SELUNET_ELAUNCH, "hipStreamDestroy failed");
+  return 0;
+}
+
+int selunet_graph_capture_begin(void* stream) {
+  SELUNET_REQUIRE(stream, "graph_capture_begin: capture needs a created (non-default) stream");
+  if (hipStreamBeginCapture(as_stream(stream), hipStreamCaptureModeThreadLocal) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipStreamBeginCapture failed");
+  return 0;
+}
+
+int selunet_graph_capture_end(void* stream, void** exec) {
+  SELUNET_REQUIRE(stream && exec, "graph_capture_end: bad arguments");
+  *exec = nullptr;
+  hipGraph_t g = nullptr;
+  if (hipStreamEndCapture(as_stream(stream), &g) != hipSuccess || !g)
+    return fail(SELUNET_ELAUNCH, "hipStreamEndCapture failed");
+  hipGraphExec_t e = nullptr;
+  const hipError_t rc = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (rc != hipSuccess) return fail(SELUNET_ELAUNCH, "hipGraphInstantiate failed");
+  *exec = e;
+  return 0;
+}
+
+int selunet_graph_launch(void* exec, void* stream) {
+  SELUNET_REQUIRE(exec, "graph_launch: bad arguments");
+  if (hipGraphLaunch((hipGraphExec_t)exec, as_stream(stream)) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipGraphLaunch failed");
+  return 0;
+}
+
+int selunet_graph_destroy(void* exec) {
+  if (exec && hipGraphExecDestroy((hipGraphExec_t)exec) != hipSuccess)
+    return fail(SELUNET_ELAUNCH, "hipGraphExecDestroy failed");
+  return 0;
+}
+
 int64_t selunet_reduce_ws_bytes(int32_t cols) { return (int64_t)RED_SPLITS * cols * (int64_t)sizeof(double); }
 
 int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* ws, double* out, float* out32,

@@ -1,0 +1,45 @@
+"""HIP-graph replay of the engine's launch plans (_lib.Plan.replay / selunet_graph_*).
+
+Once a plan has seen the same per-call buffer addresses twice, its launches run as captured HIP
+graphs. The graph path issues exactly the recorded kernels with exactly the recorded arguments, so
+a training run with graphs must be bit-identical to the same run on per-launch replay
+(SELUNET_GRAPHS=0): losses, outputs, gradients and the Adam-updated parameters."""
+import numpy as np
+import pytest
+import torch
+
+import selectivenet_for_semantic_segmentation_binary_amd as S
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
+from tests.test_gpu_model import build, train_step
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(monkeypatch, graphs, dtype, steps=5):
+    monkeypatch.setenv("SELUNET_GRAPHS", "1" if graphs else "0")
+    x, lab = make_batch(4, 64, seed=3)
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    net = build(True, dtype=dtype)
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    hist = [train_step(net, opt, xt, lt, True, 2) for _ in range(steps)]
+    eng = net._engine()
+    captured = sum(len(e.plan._graphs) + sum(len(p._graphs) for p in e.bwd.values())
+                   for lst in eng._plans.values() for e in lst if e.plan is not None)
+    params = {k: p.detach().cpu().numpy().copy() for k, p in net.named_parameters()}
+    return hist, params, captured
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graph_replay_is_bit_identical(monkeypatch, dtype):
+    h_g, p_g, n_g = _run(monkeypatch, True, dtype)
+    h_e, p_e, n_e = _run(monkeypatch, False, dtype)
+    assert n_g > 0, "no launch plan was captured into a HIP graph"
+    assert n_e == 0
+    for s, (a, b) in enumerate(zip(h_g, h_e)):
+        assert a["loss"] == b["loss"], (s, a["loss"], b["loss"])
+        assert np.array_equal(a["output"], b["output"]), s
+        for k in a["grads"]:
+            assert np.array_equal(a["grads"][k], b["grads"][k]), (s, k)
+    for k in p_g:
+        assert np.array_equal(p_g[k], p_e[k]), k
