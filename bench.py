@@ -82,7 +82,8 @@ class KernelTimer:
     dispatches to, with its algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM) and algorithmic
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
-    MFMA = ("selunet_gemm_gather", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
+    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws",
+            "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_maxpool2_fwd",
            "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
 
@@ -112,6 +113,16 @@ class KernelTimer:
             flops = 2.0 * m * n_cols * self._k(g)
             nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
             return kname, "mfma", flops, nbytes, f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
+        if name == "selunet_conv3x3_wino":  # (g, u, n_cols, ep, stream): fp32 Winograd F(2,3)
+            g, n_cols, ep = args[0], _i(args[2]), args[3]
+            kname = K.query("selunet_conv3x3_wino_kernel_name", n_cols, ep.mode, ep.split).decode()
+            m = g.n * g.h * g.w
+            c = self._k(g) // 9
+            # the MFMA work the algorithm does: 12 (dy, xi) passes per output pair = 6 per pixel
+            # (the direct 3x3 conv does 9; its FLOP count is 1.5x these)
+            flops = 2.0 * m * n_cols * 6 * c
+            nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * 12 * c * esz
+            return kname, "mfma", flops, nbytes, f"wino {g.h}x{g.w} C={c} N={n_cols} mode={ep.mode}"
         if name in ("selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to"):
             gp, gq = args[0], args[1]
             dt = _i(args[{"selunet_gemm_wgrad": 3, "selunet_gemm_wgrad_ws": 5, "selunet_gemm_wgrad_ws_to": 7}[name]])
@@ -408,10 +419,13 @@ def main():
                                    f"Adam lr=1e-3" + (f", s_lamb={args.lamb:g}" if args.selective else ""),
                        "model": model, "global_batch": args.batch, "per_gpu_batch": hi - lo, "image": args.size,
                        "parallelism": f"dp{world}",
-                       "arithmetic": "fp32 operands, exact fp32 MFMA products, fp32 accumulation"
+                       "arithmetic": "fp32 operands, exact fp32 MFMA products, fp32 accumulation; 3x3 forward and "
+                                     "data-gradient convolutions as 1-D Winograd F(2,3) with fp32 transforms"
                        if args.dtype == "fp32" else "bf16 operands, fp32 accumulation"},
             "gpu": torch.cuda.get_device_name(dev),
             "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
+            "step_flops_basis": "direct-convolution FLOPs of the training step (the fp32 Winograd layers execute "
+                                "2/3 of their share)" if args.dtype == "fp32" else "direct-convolution FLOPs",
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
             "full_loop": head.get("full_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,

@@ -125,6 +125,18 @@ int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float
  * data-gradient, conv_transpose2d forward and data-gradient (model.py:11,44,51,57). */
 int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
                         const selunet_epilogue* ep, int32_t dtype, void* stream);
+/* fp32 3x3 conv forward / data gradient (model.py:11; the reference's conv2d and its input
+ * gradient) as a 1-D Winograd F(2,3) along x: per output pair and kernel row, four fp32 MFMA passes
+ * over transformed operands (V = d0-d2, d1+d2, d2-d1, d1-d3; U = g0, (g0+g1+g2)/2, (g0-g1+g2)/2,
+ * g2) instead of six direct ones. u = [n_cols][12*C] (k = (dy*4 + xi)*C + c), written by
+ * selunet_pack_weights with kind SELUNET_PACK_CONV3X3_WINO. Same operands, epilogues and
+ * statistics slab rows (selunet_gemm_stats_rows) as selunet_gemm_gather on the same 3x3 gather;
+ * selunet_conv3x3_wino_ok tells from the shapes whether a layer can take it (fp32 multi-chunk
+ * halo layers: h, w >= 16, w even, C a multiple of 32 and > 32, n_cols a multiple of 64). */
+int32_t selunet_conv3x3_wino_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
+int selunet_conv3x3_wino(const selunet_gather* a, const float* u, int32_t n_cols,
+                         const selunet_epilogue* ep, void* stream);
+const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
 /* Rows of the stats slab selunet_gemm_gather writes for this operand (workgroup rows of the
  * kernel it dispatches to: 16x16 halo tiles for single-chunk 3x3 operands, the persistent
  * workgroups of the multi-chunk halo kernel, else 128-row tiles); -1 on error. */
@@ -173,7 +185,9 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * `offset` is computed by the call. Replaces the per-tensor loop over model.py's conv/unpool
  * parameters (model.py:11,44,51,57) that casting fp32 masters to the compute operands needs. */
 #define SELUNET_PACK_MAX 24
-enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1 };
+/* SELUNET_PACK_CONV3X3_WINO (fp32): fwd = [co][12*ci] and dgrad = [ci][12*co] Winograd weight
+ * operands of selunet_conv3x3_wino (k_pad = 12*ci; dgrad from the flipped/transposed kernel). */
+enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1, SELUNET_PACK_CONV3X3_WINO = 2 };
 typedef struct selunet_pack_desc {
   const float* w;
   void* fwd;

@@ -48,7 +48,7 @@ class PackDesc(ctypes.Structure):
                 ("ci", c_int32), ("k_pad", c_int32), ("offset", c_int64)]
 
 
-PACK_MAX, PACK_CONV3X3, PACK_CONVT = 24, 0, 1
+PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO = 24, 0, 1, 2
 WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
 
 
@@ -83,6 +83,9 @@ SIGNATURES = {
     "selunet_gemm_wgrad_ws": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, P, c_int64, c_int32, P]),
     "selunet_gemm_wgrad_ws_to": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, P, c_int64, c_int32, P,
                                            c_int32, P]),
+    "selunet_conv3x3_wino_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "selunet_conv3x3_wino": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P]),
+    "selunet_conv3x3_wino_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
     "selunet_set_gather_workgroups": (c_int32, [c_int32]),

@@ -588,6 +588,296 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3);
 }
 
+// =========================================================================== fp32 Winograd F(2,3)
+// fp32 forward / data gradient of the multi-chunk layers as a 1-D Winograd F(2,3) along x: for each
+// kernel row dy, a pair of outputs (x, x+1) is
+//   y(x)   = M0 + M1 + M2,   y(x+1) = M1 - M2 - M3,   M_xi = sum_c U_xi[dy][c] * V_xi[c]
+// with V0 = d0 - d2, V1 = d1 + d2, V2 = d2 - d1, V3 = d1 - d3 (d_j = input at x - 1 + j, row y + dy)
+// and U0 = g0, U1 = (g0 + g1 + g2) / 2, U2 = (g0 - g1 + g2) / 2, U3 = g2 (the kernel row's taps,
+// transformed once per step by selunet_pack_weights). Per output pixel that is 3 x 4 / 2 = 6 fp32
+// MFMA k-passes over the input channels instead of 9: the exact-fp32 MFMA work drops by 1.5x; the
+// transforms are one fp32 add per operand element (rounding comparable to the direct sum: measured
+// relative RMS 3.1e-7 vs 1.8e-7 direct at C = 512, fp64 reference).
+// Structure as conv3x3_halo_persist_kernel (persistent column-tile walk, halo prefetch across the
+// epilogue, statistics in registers) with 12 steps (dy, xi) per 32-channel chunk. The halo tile's
+// columns are stored deinterleaved by parity (even x first), so the d_j reads of a wave's 32 output
+// pairs (8 pairs x 4 rows) are 4 runs of 8 consecutive LDS rows, as the direct kernel's reads.
+// Waves: 4 (pair rows) x 2 (column halves of BN); accumulators acc[xi][BN/64] per wave.
+constexpr int WINO_STEPS = 12;
+__device__ __forceinline__ int wino_row(int hp) {
+  const int hy = hp / HWT, hx = hp - hy * HWT;
+  return hy * HWT + (hx & 1) * (HWT / 2) + (hx >> 1);
+}
+
+template <int BN>
+__global__ void __launch_bounds__(HTHREADS, 1)
+conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles,
+                            int tiles_x, int tiles_y, int ptiles, int gp) {
+  using T = float;
+  constexpr int E = 4;
+  constexpr int CK = 32;
+  constexpr int NT = BN / 64;  // 32-column subtiles per wave
+  constexpr int B_ROUNDS = BN * 8 / HTHREADS;
+  static_assert(B_ROUNDS * HTHREADS == BN * 8, "weight tile rows must split evenly over the threads");
+  static_assert(A_ROUNDS <= 6, "halo slice schedule covers six slices");
+
+  constexpr int SMEM_MAIN = 2 * HPIX * AROWB + 2 * BN * ROWB + 2 * CK * 8;
+  constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + 2 * HPIX * AROWB;
+  float* Ss = reinterpret_cast<float*>(Bs + 2 * BN * ROWB);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+  // this lane's output pair: tile row py, pixels 2 px2 and 2 px2 + 1
+  const int pair = wm * 32 + l32, py = pair >> 3, px2 = pair & 7;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n_tile = lb % n_tiles;
+  const int prow = lb / n_tiles;
+  const int n0 = n_tile * BN;
+  const int ntl = prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0;
+  const int nchunks = g.Ctot / CK;
+  const int csteps = nchunks * WINO_STEPS;
+
+  auto tile_xy = [&](int i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned pt = (unsigned)(prow + i * gp);
+    const unsigned r = pt / (unsigned)tiles_x;
+    x0 = (int)(pt - r * (unsigned)tiles_x) * TW;
+    const unsigned r2 = r / (unsigned)tiles_y;
+    y0 = (int)(r - r2 * (unsigned)tiles_y) * TH;
+    img = (int)r2;
+  };
+  auto a_slot = [&](int round, int& hp, int& cc) -> bool {
+    const int hidx = round * HTHREADS + tid;
+    hp = min(hidx >> 3, HPIX - 1);
+    cc = hidx & 7;
+    return hidx < HPIX * 8;
+  };
+  auto a_inside = [&](int y0, int x0, int hp) -> bool {
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    return (unsigned)(y0 - 1 + hy) < (unsigned)g.h && (unsigned)(x0 - 1 + hx) < (unsigned)g.w;
+  };
+  auto chunk_src = [&](int chunk, int& c) -> SrcArg {
+    c = chunk * CK;
+    const bool s1 = g.nsrc > 1 && c >= g.src[0].C;
+    if (s1) c -= g.src[0].C;
+    return pick_src(g, s1 ? 1 : 0);
+  };
+  auto a_ptr = [&](const SrcArg& sa, int c, int img, int y0, int x0, int hp, int cc) -> const uint4* {
+    const int hy = hp / HWT, hx = hp - (hp / HWT) * HWT;
+    const int ys = min(max(y0 - 1 + hy, 0), g.h - 1), xs = min(max(x0 - 1 + hx, 0), g.w - 1);
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(sa.data) +
+                                          (((int64_t)img * g.h + ys) * g.w + xs) * sa.C + c + cc * E);
+  };
+  struct BRegs {
+    uint4 v[B_ROUNDS];
+  };
+  auto b_load = [&](int st) __attribute__((always_inline)) {  // st: step within a tile
+    const int chunk = st / WINO_STEPS, t = st - chunk * WINO_STEPS;
+    const int k0 = t * g.Ctot + chunk * CK;
+    BRegs rb;
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      rb.v[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
+    }
+    return rb;
+  };
+  auto b_store = [&](const BRegs& rb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < B_ROUNDS; ++r) {
+      const int idx = r * HTHREADS + tid;
+      const int row = idx >> 3, cc = idx & 7;
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb.v[r];
+    }
+  };
+
+  f32x16 acc[4][NT];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[x][b] = f32x16{};
+  const int prow0 = py * HWT + px2;  // LDS row of d_0 at dy = 0
+
+  // step t = (dy, xi): V_xi from two d_j rows of the halo, one MFMA pass per column subtile
+  auto mma_step = [&](int hbuf, int bbuf, int t) __attribute__((always_inline)) {
+    const unsigned char* a_src = As + hbuf * HPIX * AROWB;
+    const unsigned char* b_src = Bs + bbuf * BN * ROWB;
+    const int dy = t >> 2, xi = t & 3;
+    const int ja = xi == 0 ? 0 : (xi == 2 ? 2 : 1);
+    const int jb = xi == 3 ? 3 : (xi == 2 ? 1 : 2);
+    const int sw = ((half ^ (py + dy)) & 1) * 16;
+    const unsigned char* pa = a_src + (prow0 + dy * HWT + (ja & 1) * (HWT / 2) + (ja >> 1)) * AROWB + sw;
+    const unsigned char* pb = a_src + (prow0 + dy * HWT + (jb & 1) * (HWT / 2) + (jb >> 1)) * AROWB + sw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 da = *reinterpret_cast<const float4*>(pa + q * 32);
+      const float4 db = *reinterpret_cast<const float4*>(pb + q * 32);
+      uint4 bfr[NT];
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * (BN / 2) + b * 32 + l32) * ROWB + q * 32 + half * 16);
+      float4 v;
+      if (xi == 1) v = make_float4(da.x + db.x, da.y + db.y, da.z + db.z, da.w + db.w);
+      else v = make_float4(da.x - db.x, da.y - db.y, da.z - db.z, da.w - db.w);
+      const uint4 av = make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
+#pragma unroll
+      for (int b = 0; b < NT; ++b) Mma<float>::run(acc[xi][b], av, bfr[b]);
+    }
+  };
+  auto halo_put_global = [&](uint4 v, int r, const SrcArg& sa, int c, int y0, int x0, int hb)
+      __attribute__((always_inline)) {
+    int hp, cc;
+    if (!a_slot(r, hp, cc)) return;
+    uint4 o = make_uint4(0, 0, 0, 0);
+    if (a_inside(y0, x0, hp)) o = sa.scale ? transform16<T>(v, sa.scale, sa.shift, c + cc * E, sa.relu) : v;
+    *reinterpret_cast<uint4*>(As + hb * HPIX * AROWB + halo_off(wino_row(hp), cc)) = o;
+  };
+
+  // ---------------------------------------------------------------- prologue: tile 0 chunk 0, B(0), B(1)
+  {
+    int img, y0, x0;
+    tile_xy(0, img, y0, x0);
+    int c0;
+    const SrcArg sa = chunk_src(0, c0);
+    uint4 v0[A_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) {
+      int hp, cc;
+      a_slot(r, hp, cc);
+      v0[r] = *a_ptr(sa, c0, img, y0, x0, hp, cc);
+    }
+#pragma unroll
+    for (int r = 0; r < A_ROUNDS; ++r) halo_put_global(v0[r], r, sa, c0, y0, x0, 0);
+  }
+  BRegs rb_next = b_load(0);
+  b_store(rb_next, 0);
+  rb_next = b_load(1 % csteps);
+  __syncthreads();
+
+  using Acc = typename StatAcc<T>::type;
+  static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
+  Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const TileStats ts = tile_stats(ep, prow, n0, N);
+  float* tile = reinterpret_cast<float*>(smem);
+  uint4 ra[A_ROUNDS];
+  int J = 0;
+  int S = 0;
+  for (int i = 0; i < ntl; ++i) {
+    int img, y0, x0;
+    tile_xy(i, img, y0, x0);
+    BRegs rb_hold;
+    for (int c = 0; c < nchunks; ++c, ++J) {
+      const bool last_c = c + 1 == nchunks;
+      const bool has_next = !last_c || i + 1 < ntl;
+      const bool defer = last_c && has_next;
+      int nimg = img, ny0 = y0, nx0 = x0;
+      if (defer) tile_xy(i + 1, nimg, ny0, nx0);
+      const int nc = !has_next ? c : (last_c ? 0 : c + 1);
+      int cs;
+      const SrcArg sn = chunk_src(nc, cs);
+      float* ssc = Ss + ((J + 1) & 1) * CK;
+      float* ssh = Ss + 2 * CK + ((J + 1) & 1) * CK;
+      float coef = 0.0f;
+#pragma unroll
+      for (int t = 0; t < WINO_STEPS; ++t) {
+        const int st2 = c * WINO_STEPS + t + 2;
+        const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);
+        if (t == 0 && !defer && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
+#pragma unroll
+        for (int r = 0; r < A_ROUNDS; ++r) {
+          if (r == t) {
+            int hp, cc;
+            a_slot(r, hp, cc);
+            ra[r] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
+          }
+        }
+        mma_step(J & 1, S & 1, t);
+        if (defer && t == WINO_STEPS - 1) rb_hold = rb_next;
+        else b_store(rb_next, (S + 1) & 1);
+        if (!defer) {
+          if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
+#pragma unroll
+          for (int r = 0; r < A_ROUNDS; ++r) {
+            if (r + 3 != t) continue;
+            int hp, cc;
+            if (a_slot(r, hp, cc)) {
+              uint4 v = make_uint4(0, 0, 0, 0);
+              if (a_inside(ny0, nx0, hp)) {
+                v = ra[r];
+                if (sn.scale) {
+                  float e[E];
+                  __builtin_memcpy(e, &v, 16);
+#pragma unroll
+                  for (int j = 0; j < E; ++j) {
+                    float f = e[j] * ssc[cc * E + j] + ssh[cc * E + j];
+                    if (sn.relu) f = fmaxf(f, 0.0f);
+                    e[j] = f;
+                  }
+                  __builtin_memcpy(&v, e, 16);
+                }
+              }
+              *reinterpret_cast<uint4*>(As + ((J + 1) & 1) * HPIX * AROWB + halo_off(wino_row(hp), cc)) = v;
+            }
+          }
+        }
+        __syncthreads();
+        rb_next = rb_far;
+        ++S;
+      }
+    }
+
+    // ------------------------------------------------------------ epilogue of tile i
+    // output transform in registers (the lane holds all four M_xi of its pairs), pixels -> LDS
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int col = wn * (BN / 2) + b * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const int e = (pr >> 3) * TW + 2 * (pr & 7);
+        const float m0 = acc[0][b][r], m1 = acc[1][b][r], m2 = acc[2][b][r], m3 = acc[3][b][r];
+        tile[e * (BN + 4) + col] = (m0 + m1) + m2;
+        tile[(e + 1) * (BN + 4) + col] = (m1 - m2) - m3;
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[x][b] = f32x16{};
+    __syncthreads();
+    auto dst = [&](int pix, int cl) -> T* {
+      const int y = y0 + pix / TW, x = x0 + pix % TW;
+      if (y >= g.h || x >= g.w) return nullptr;
+      const int64_t m = ((int64_t)img * g.h + y) * g.w + x;
+      const int col = n0 + cl;
+      if (ep.mode == SELUNET_EP_SPLIT)
+        return col < ep.split ? reinterpret_cast<T*>(ep.out0) + m * ep.split + col
+                              : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
+      return reinterpret_cast<T*>(ep.out0) + m * N + col;
+    };
+    auto bias_col = [&](int cl) { return n0 + cl; };
+    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+    if (i + 1 < ntl) {
+      __syncthreads();
+      int nimg, ny0, nx0;
+      tile_xy(i + 1, nimg, ny0, nx0);
+      int cs;
+      const SrcArg sn = chunk_src(0, cs);
+#pragma unroll
+      for (int r = 0; r < A_ROUNDS; ++r) halo_put_global(ra[r], r, sn, cs, ny0, nx0, J & 1);
+      b_store(rb_hold, S & 1);
+      __syncthreads();
+    }
+  }
+  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3);
+}
+
 // =========================================================================== weight gradient
 // dW[co][tap][ci] = sum_p dY[p][co] * X[p + off(tap)][ci] for one co tile (BI) and one 64-channel
 // ci chunk, reduced over the pixel tiles (8 x 16) of a split; fp32 atomics at the end.
@@ -1159,6 +1449,43 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N, k_pad,
                      ep, n_tiles, tiles_x, tiles_y);
+}
+
+static bool wino_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("SELUNET_WINO");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+bool conv3x3_wino_shape_ok(int h, int w, int c_in, int c_src0, int n_cols) {
+  return wino_enabled() && persist_enabled() && h >= TH && w >= TW && w % 2 == 0 && c_in % 32 == 0 &&
+         c_src0 % 32 == 0 && c_in > 32 && n_cols % 64 == 0;
+}
+
+bool conv3x3_wino_eligible(const GatherArg& g, int N) {
+  return conv3x3_halo_eligible(g, N, SELUNET_F32) && conv3x3_halo_persistent(g, SELUNET_F32) &&
+         conv3x3_wino_shape_ok(g.h, g.w, g.Ctot, g.src[0].C, N);
+}
+
+template <int BN>
+static void launch_wino(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st) {
+  const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
+  const int n_tiles = N / BN;
+  const int gp = persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
+  hipLaunchKernelGGL((conv3x3_wino_persist_kernel<BN>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, u,
+                     N, WINO_STEPS * g.Ctot, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp);
+}
+
+bool conv3x3_wino_bn128(int N, const EpiArg& ep) {
+  return N % 128 == 0 && !(ep.mode == SELUNET_EP_SPLIT && ep.split % 128 != 0);
+}
+
+int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st) {
+  if (conv3x3_wino_bn128(N, ep)) launch_wino<128>(g, u, N, ep, st);
+  else launch_wino<64>(g, u, N, ep, st);
+  return check_launch("conv3x3_wino");
 }
 
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,

@@ -857,12 +857,12 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
   return bf ? "gemm_wgrad_bf16" : "gemm_wgrad<f32>";
 }
 
-extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
-                                   const selunet_epilogue* ep, int32_t dtype, void* stream) {
+// Argument checks shared by selunet_gemm_gather and selunet_conv3x3_wino; fills g and e.
+static int check_gather_call(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
+                             const selunet_epilogue* ep, int32_t dtype, GatherArg& g, EpiArg& e) {
   SELUNET_REQUIRE(dtype == SELUNET_F32 || dtype == SELUNET_BF16, "dtype must be SELUNET_F32 or SELUNET_BF16");
   const int esz = dtype == SELUNET_F32 ? 4 : 2;
   const int bke = 128 / esz;
-  GatherArg g;
   if (int rc = make_gather(a, dtype, g, 16 / esz)) return rc;
   SELUNET_REQUIRE(b != nullptr && ep != nullptr && ep->out0 != nullptr, "B / epilogue / out0 must be non-NULL");
   SELUNET_REQUIRE(n_cols > 0 && n_cols % 64 == 0, "n_cols must be a positive multiple of 64 (got %d)", n_cols);
@@ -883,8 +883,16 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
     SELUNET_REQUIRE(ep->mode == SELUNET_EP_PLAIN && ep->stats == nullptr && bb.y && bb.scale && bb.shift && bb.mean &&
                         bb.invstd && ep->bias == nullptr,
                     "bn-backward sums need the plain epilogue without stats/bias and y/scale/shift/mean/invstd");
-  EpiArg e{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split, ep->colsum,
-           BnBwdArg{bb.y, bb.scale, bb.shift, bb.mean, bb.invstd, bb.slab}};
+  e = EpiArg{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split, ep->colsum,
+             BnBwdArg{bb.y, bb.scale, bb.shift, bb.mean, bb.invstd, bb.slab}};
+  return SELUNET_OK;
+}
+
+extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32_t n_cols, int32_t k_pad,
+                                   const selunet_epilogue* ep, int32_t dtype, void* stream) {
+  GatherArg g;
+  EpiArg e;
+  if (int rc = check_gather_call(a, b, n_cols, k_pad, ep, dtype, g, e)) return rc;
   hipStream_t st = as_stream(stream);
   if (ep->mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype))
     return conv3x3_halo_launch(g, b, n_cols, k_pad, e, dtype, st);
@@ -897,6 +905,32 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
     else launch_gather<__bf16, 64>(g, b, n_cols, k_pad, e, st);
   }
   return check_launch("gemm_gather");
+}
+
+extern "C" int32_t selunet_conv3x3_wino_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols) {
+  return halo_enabled() && conv3x3_wino_shape_ok(h, w, c_in, c_src0, n_cols) ? 1 : 0;
+}
+
+extern "C" const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32_t split) {
+  EpiArg e{};
+  e.mode = mode;
+  e.split = split;
+  return conv3x3_wino_bn128(n_cols, e) ? "conv3x3_wino<f32,128>" : "conv3x3_wino<f32,64>";
+}
+
+extern "C" int selunet_conv3x3_wino(const selunet_gather* a, const float* u, int32_t n_cols,
+                                   const selunet_epilogue* ep, void* stream) {
+  GatherArg g;
+  EpiArg e;
+  SELUNET_REQUIRE(a != nullptr && a->taps == 9, "conv3x3_wino: a 3x3 (taps = 9) gather is required");
+  if (int rc = check_gather_call(a, u, n_cols, 12 * a->src[0].channels + 12 * (a->nsrc > 1 ? a->src[1].channels : 0),
+                                 ep, SELUNET_F32, g, e))
+    return rc;
+  SELUNET_REQUIRE(ep->mode != SELUNET_EP_SCATTER2X, "conv3x3_wino: scatter epilogue not supported");
+  SELUNET_REQUIRE(halo_enabled() && conv3x3_wino_eligible(g, n_cols),
+                  "conv3x3_wino: operand not eligible (%dx%d, C=%d, n_cols=%d; see selunet_conv3x3_wino_ok)", g.h, g.w,
+                  g.Ctot, n_cols);
+  return conv3x3_wino_launch(g, u, n_cols, e, as_stream(stream));
 }
 
 // Deterministic split reduction of the weight-gradient partials: out[i][j] = sum_s ws[s][i][j]

@@ -407,6 +407,11 @@ int64_t conv3x3_halo_stats_rows(const GatherArg& g, int N, int dtype);  // slab 
 bool conv3x3_halo_persistent(const GatherArg& g, int dtype);            // multi-chunk: persistent kernel
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st);
+// fp32 1-D Winograd F(2,3) forward / data gradient (conv3x3.hip, selunet_conv3x3_wino)
+bool conv3x3_wino_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
+bool conv3x3_wino_eligible(const GatherArg& g, int N);
+bool conv3x3_wino_bn128(int N, const EpiArg& ep);
+int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
                               hipStream_t st);

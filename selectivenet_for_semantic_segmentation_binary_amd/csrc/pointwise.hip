@@ -125,6 +125,22 @@ __global__ void pack_weights_kernel(selunet_pack_list l, int64_t total) {
         const int tap = k / co, o = k - tap * co;
         dg[q] = from_f<T>(w[((int64_t)o * ci + c) * 9 + (8 - tap)]);
       }
+    } else if (d.kind == SELUNET_PACK_CONV3X3_WINO) {  // fp32 Winograd F(2,3) operands (conv3x3.hip)
+      const int co = d.co, ci = d.ci;
+      const int64_t total_f = (int64_t)co * 12 * ci;
+      const bool fw = j < total_f;
+      const int64_t q = fw ? j : j - total_f;
+      const int rows_k = fw ? ci : co;  // k = (dy*4 + xi)*rows_k + c
+      const int r = (int)(q / (12 * rows_k));
+      const int k = (int)(q % (12 * rows_k));
+      const int t = k / rows_k, c = k - t * rows_k;
+      const int dy = t >> 2, xi = t & 3;
+      // fwd: row o = r, input channel c, kernel row dy; dgrad: row = input channel r, column o = c,
+      // flipped kernel (row 2 - dy, taps 2 - j)
+      const float* gw = fw ? w + ((int64_t)r * ci + c) * 9 + dy * 3 : w + ((int64_t)c * ci + r) * 9 + (2 - dy) * 3;
+      const double g0 = fw ? gw[0] : gw[2], g1 = gw[1], g2 = fw ? gw[2] : gw[0];
+      const double u = xi == 0 ? g0 : xi == 1 ? 0.5 * (g0 + g1 + g2) : xi == 2 ? 0.5 * (g0 - g1 + g2) : g2;
+      (fw ? fwd : dg)[q] = from_f<T>((float)u);
     } else {  // as pack_convT_kernel: w[c][o][ab]
       const int ci = d.ci, co = d.co;
       const int ab = (int)(j & 3);
@@ -1163,6 +1179,10 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
     if (d.kind == SELUNET_PACK_CONV3X3) {
       SELUNET_REQUIRE(d.fwd && d.k_pad >= 9 * d.ci, "pack_weights: bad conv3x3 entry %d", t);
       off += (int64_t)d.co * d.k_pad + (d.dgrad ? (int64_t)d.ci * 9 * d.co : 0);
+    } else if (d.kind == SELUNET_PACK_CONV3X3_WINO) {
+      SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == 12 * d.ci,
+                      "pack_weights: Winograd entry %d needs fp32, fwd and k_pad = 12*ci", t);
+      off += (int64_t)d.co * 12 * d.ci + (d.dgrad ? (int64_t)d.ci * 12 * d.co : 0);
     } else {
       SELUNET_REQUIRE(d.kind == SELUNET_PACK_CONVT, "pack_weights: bad kind in entry %d", t);
       off += (int64_t)d.ci * d.co * 4;

@@ -157,37 +157,64 @@ class Engine:
         else:
             K.call("selunet_unpack_convT_grad", K.ptr(packed), ni, out.shape[1], K.ptr(out), self.stream)
 
-    def pack_weights(self, P, need_dgrad=True):
-        """fp32 master weights -> GEMM operand layouts in the compute dtype (one launch for all)."""
+    def _wino_ok(self, name, ci, co, hw, need_dgrad):
+        """fp32 layers whose forward (and data gradient) run as the Winograd F(2,3) kernel
+        (selunet_conv3x3_wino): decided from the layer's resolution and channels."""
+        if self.dt != torch.float32 or hw is None or name == "encoder_layer_1_1":
+            return False
+        f = 1 << (int(name.split("_")[2]) - 1)  # encoder/decoder level k runs at 1 / 2^(k-1)
+        h, w = hw[0] // f, hw[1] // f
+        concat = name.startswith("decoder_layer") and name.endswith("_2") and name != "decoder_layer_4_2"
+        c0 = ci // 2 if concat else ci  # torch.cat((unpool, skip)) inputs: two equal sources
+        ok = K.query("selunet_conv3x3_wino_ok", h, w, ci, c0, co) == 1
+        return ok and (not need_dgrad or K.query("selunet_conv3x3_wino_ok", h, w, co, co, ci) == 1)
+
+    def pack_weights(self, P, need_dgrad=True, hw=None):
+        """fp32 master weights -> GEMM operand layouts in the compute dtype (one launch for all);
+        fp32 layers at input resolution hw that the Winograd kernel takes get its U operands.
+        Returns name -> (fwd, dgrad, k_pad or ci, winograd)."""
         dev = P["encoder_layer_1_2.0.weight"].device
         packs = {}
         pl = K.PackList()
         for name, ci, co in LY.CBR_LAYERS:
             w = P[f"{name}.0.weight"]
             ci = w.shape[1]
-            kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
+            wino = self._wino_ok(name, ci, co, hw, need_dgrad)
+            if wino:
+                kpad, taps, kind = 12 * ci, 12, K.PACK_CONV3X3_WINO
+            else:
+                kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
+                taps, kind = 9, K.PACK_CONV3X3
             fwd = K.keep(torch.empty(co, kpad, dtype=self.dt, device=dev))
             dg = None
             if need_dgrad and name != "encoder_layer_1_1":
-                dg = K.keep(torch.empty(ci, 9 * co, dtype=self.dt, device=dev))
-            pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONV3X3, co, ci, kpad, 0)
+                dg = K.keep(torch.empty(ci, taps * co, dtype=self.dt, device=dev))
+            pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), kind, co, ci, kpad, 0)
             pl.n += 1
-            packs[name] = (fwd, dg, kpad)
+            packs[name] = (fwd, dg, kpad, wino)
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
             fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
             dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
             pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
             pl.n += 1
-            packs[name] = (fwd, dg, ci)
+            packs[name] = (fwd, dg, ci, False)
         K.call("selunet_pack_weights", pl, self.code, self.stream)
         return packs
 
     # ------------------------------------------------------------------ forward pieces
+    def _conv3x3(self, g, b, n_cols, kpad, ep, wino):
+        """A 3x3 conv (forward or data gradient) through the direct halo / gather kernels, or the
+        fp32 Winograd kernel when the layer's operands were packed for it."""
+        if wino:
+            K.call("selunet_conv3x3_wino", g, K.ptr(b), n_cols, ep, self.stream)
+        else:
+            K.call("selunet_gemm_gather", g, K.ptr(b), n_cols, kpad, ep, self.code, self.stream)
+
     def _cbr(self, ctx, name, P, B, n, h, w, *srcs, taps=9, first_x=None):
         """CBR_2D forward (model.py:9-15): conv (+ BN batch statistics in its epilogue), BN finalize.
         first_x: the network input (NCHW fp32) for encoder_layer_1_1, convolved directly."""
-        fwd, _, kpad = ctx.wpack[name]
+        fwd, _, kpad, wino = ctx.wpack[name]
         co = fwd.shape[0]
         M = n * h * w
         dev = fwd.device
@@ -205,7 +232,7 @@ class Engine:
                    K.ptr(stats), self.code, self.stream)
         else:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
-            K.call("selunet_gemm_gather", g, K.ptr(fwd), co, kpad, ep, self.code, self.stream)
+            self._conv3x3(g, fwd, co, kpad, ep, wino)
         mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
         if ctx.training and self.dt == torch.float32:
             # fp32 (parity): two-pass statistics — the epilogue's sums give the batch mean, a second
@@ -248,7 +275,7 @@ class Engine:
         return out
 
     def _up(self, ctx, name, P, st: BNState):
-        fwd, _, ci = ctx.wpack[name]
+        fwd, _, ci, _ = ctx.wpack[name]
         co = fwd.shape[0] // 4
         out = K.keep(torch.empty(st.n * 2 * st.h * 2 * st.w, co, dtype=self.dt, device=st.y.device))
         g = K.gather(st.n, st.h, st.w, 1, st.src())
@@ -326,7 +353,7 @@ class Engine:
         n, cin, H, W = x.shape
         ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
         ctx.ce_heads = ce_heads
-        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward)
+        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W))
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
         h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
         # first layer (C_in = 3 or 2): convolved straight from the NCHW fp32 input
@@ -440,7 +467,7 @@ class Engine:
         K.marker(("grads", name))
         if not need_dgrad:
             return None
-        _, wd, _ = ctx.wpack[name]
+        _, wd, _, wino = ctx.wpack[name]
         ga = K.gather(st.n, st.h, st.w, 9, K.source(dy, co))
         rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
         if dgrad_split is None:
@@ -450,20 +477,20 @@ class Engine:
             if prev is not None:
                 slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
                 ep.bnb = bnb_for(prev, slab)
-            K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
+            self._conv3x3(ga, wd, ci, 9 * co, ep, wino)
             return DGrad(dx, slab, rows)
         c0 = dgrad_split
         d0 = K.keep(torch.empty(M, c0, dtype=self.dt, device=dev))
         d1 = K.keep(torch.empty(M, ci - c0, dtype=self.dt, device=dev))
         colsum = K.keep(torch.empty(rows, c0, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0, K.ptr(colsum))
-        K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 9 * co, ep, self.code, self.stream)
+        self._conv3x3(ga, wd, ci, 9 * co, ep, wino)
         return DGrad(d0, colsum, rows), d1
 
     def _up_bwd(self, ctx, name, du: DGrad, G, prev: BNState):
         """ConvTranspose2d(k2,s2) backward: bias (from du's column sums), weight and data gradients;
         the data gradient carries prev's BN-backward sums."""
-        fwd, wd, ci = ctx.wpack[name]
+        fwd, wd, ci, _ = ctx.wpack[name]
         co = fwd.shape[0] // 4
         n, h, w = prev.n, prev.h, prev.w
         dev = du.t.device

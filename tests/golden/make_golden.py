@@ -631,9 +631,9 @@ if __name__ == "__main__":
         big_fixtures()
         sys.exit(0)
     if sys.argv[1:2] == ["ensemble"]:
+        big = lambda f: "n128" in f or "n8_512" in f  # noqa: E731
         for f in sys.argv[2:]:
-            augment_ensemble(f, k_members=8 if "n128" not in f and "n8_512" not in f else 3,
-                             ckpt="n128" in f or "n8_512" in f)
+            augment_ensemble(f, k_members=int(os.environ.get("ENS_MEMBERS", 3 if big(f) else 8)), ckpt=big(f))
         sys.exit(0)
     if sys.argv[1:] == ["big512"]:
         big512()

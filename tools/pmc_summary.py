@@ -14,24 +14,40 @@ import re
 import sys
 from collections import defaultdict
 
-# rocprofv3 kernel-name pattern -> selunet kernel name
-NAME_MAP = [
-    (r"conv3x3_halo_persist_kernelIDF16bLi128", "conv3x3_halo_persist<bf16,128>"),
-    (r"conv3x3_halo_persist_kernelIDF16bLi64", "conv3x3_halo_persist<bf16,64>"),
-    (r"conv3x3_halo_persist_kernelIfLi128", "conv3x3_halo_persist<f32,128>"),
-    (r"conv3x3_halo_persist_kernelIfLi64", "conv3x3_halo_persist<f32,64>"),
-    (r"conv3x3_halo_kernelIDF16bLi64ELb1", "conv3x3_halo1<bf16,64>"),
-    (r"conv3x3_halo_kernelIfLi64ELb1", "conv3x3_halo1<f32,64>"),
-    (r"conv3x3_halo_kernelIDF16bLi128", "conv3x3_halo<bf16,128>"),
-    (r"conv3x3_halo_kernelIDF16bLi64", "conv3x3_halo<bf16,64>"),
-    (r"conv3x3_halo_kernelIfLi128", "conv3x3_halo<f32,128>"),
-    (r"conv3x3_halo_kernelIfLi64", "conv3x3_halo<f32,64>"),
-    (r"conv3x3_wgrad_halo_f32_kernelILi128", "conv3x3_wgrad_halo_f32<128>"),
-    (r"conv3x3_wgrad_halo_f32_kernelILi64", "conv3x3_wgrad_halo_f32<64>"),
-    (r"conv3x3_wgrad_halo_kernel<128>|conv3x3_wgrad_halo_kernelILi128", "conv3x3_wgrad_halo<128>"),
-    (r"conv3x3_wgrad_halo_kernel<64>|conv3x3_wgrad_halo_kernelILi64", "conv3x3_wgrad_halo<64>"),
-    (r"gemm_gather_kernelIDF16b", "gemm_gather<bf16>"),
-    (r"gemm_gather_kernelIf", "gemm_gather<f32>"),
+# rocprofv3 kernel-name pattern -> selunet kernel name (as bench.py names them). rocprofv3 prints
+# fp32 instantiations demangled ("conv3x3_halo_persist_kernel<float, 128>") and bf16 ones mangled
+# ("conv3x3_halo_persist_kernelIDF16bLi128E"): every entry matches both spellings.
+_MANGLE = {"bf16": ("DF16b", "__bf16"), "f32": ("f", "float"), "true": ("Lb1E", "true")}
+
+
+def _pat(base, *targs):
+    m = "".join(_MANGLE[a][0] if a in _MANGLE else f"Li{a}E" for a in targs)
+    d = ", ".join(_MANGLE[a][1] if a in _MANGLE else str(a) for a in targs)
+    return rf"{base}I{m}|{re.escape(base + '<' + d)}[,>]" if targs else base
+
+
+NAME_MAP = []
+for _t in ("bf16", "f32"):
+    NAME_MAP += [
+        (_pat("conv3x3_halo_persist_kernel", _t, 128), f"conv3x3_halo_persist<{_t},128>"),
+        (_pat("conv3x3_halo_persist_kernel", _t, 64), f"conv3x3_halo_persist<{_t},64>"),
+        (_pat("conv3x3_halo_kernel", _t, 64, "true"), f"conv3x3_halo1<{_t},64>"),
+        (_pat("conv3x3_halo_kernel", _t, 128), f"conv3x3_halo<{_t},128>"),
+        (_pat("conv3x3_halo_kernel", _t, 64), f"conv3x3_halo<{_t},64>"),
+        (_pat("gemm_gather_kernel", _t), f"gemm_gather<{_t}>"),
+        (_pat("bn_bwd_apply_kernel", _t), f"bn_bwd_apply<{_t}>"),
+        (_pat("maxpool_fwd_kernel", _t), f"maxpool2_fwd<{_t}>"),
+        (_pat("maxpool_bwd_kernel", _t), f"maxpool2_bwd<{_t}>"),
+        (_pat("heads_fwd_kernel", _t), f"heads_fwd<{_t}>"),
+        (_pat("heads_bwd_kernel", _t), f"heads_bwd<{_t}>"),
+        (_pat("first_conv_fwd_kernel", _t), f"first_conv_fwd<{_t}>"),
+        (_pat("first_conv_wgrad_kernel", _t), f"first_conv_wgrad<{_t}>"),
+    ]
+NAME_MAP += [
+    (_pat("conv3x3_wgrad_halo_f32_kernel", 128), "conv3x3_wgrad_halo_f32<128>"),
+    (_pat("conv3x3_wgrad_halo_f32_kernel", 64), "conv3x3_wgrad_halo_f32<64>"),
+    (_pat("conv3x3_wgrad_halo_kernel", 128), "conv3x3_wgrad_halo<128>"),
+    (_pat("conv3x3_wgrad_halo_kernel", 64), "conv3x3_wgrad_halo<64>"),
     (r"gemm_wgrad_bf16_kernel", "gemm_wgrad_bf16"),
     (r"gemm_wgrad_kernel", "gemm_wgrad<f32>"),
 ]
