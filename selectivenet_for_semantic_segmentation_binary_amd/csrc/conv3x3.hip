@@ -609,7 +609,9 @@ __device__ __forceinline__ int wino_row(int hp) {
   return hy * HWT + (hx & 1) * (HWT / 2) + (hx >> 1);
 }
 
-template <int BN>
+// XS = transformed planes (xi) per step: 1 (BN = 128: 12 steps per chunk) or 2 (BN = 64: 6 steps,
+// so a step carries as many MFMAs per barrier as the BN = 128 one; two planes of weights per buffer)
+template <int BN, int XS>
 __global__ void __launch_bounds__(HTHREADS, 1)
 conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles,
                             int tiles_x, int tiles_y, int ptiles, int gp) {
@@ -617,16 +619,21 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
   constexpr int E = 4;
   constexpr int CK = 32;
   constexpr int NT = BN / 64;  // 32-column subtiles per wave
-  constexpr int B_ROUNDS = BN * 8 / HTHREADS;
-  static_assert(B_ROUNDS * HTHREADS == BN * 8, "weight tile rows must split evenly over the threads");
+  constexpr int STEPS = WINO_STEPS / XS;
+  constexpr int BROWS = XS * BN;  // weight rows per step (plane-major)
+  constexpr int B_ROUNDS = BROWS * 8 / HTHREADS;
+  static_assert(XS == 1 || XS == 2, "one or two planes per step");
+  // halo slice r of the next job: loaded at step lt(r), written to LDS at lt(r) + 3
+  auto lt = [](int r) { return XS == 1 ? r : r >> 1; };
+  static_assert(B_ROUNDS * HTHREADS == BROWS * 8, "weight tile rows must split evenly over the threads");
   static_assert(A_ROUNDS <= 6, "halo slice schedule covers six slices");
 
-  constexpr int SMEM_MAIN = 2 * HPIX * AROWB + 2 * BN * ROWB + 2 * CK * 8;
+  constexpr int SMEM_MAIN = 2 * HPIX * AROWB + 2 * BROWS * ROWB + 2 * CK * 8;
   constexpr int SMEM_EPI = TH * TW * (BN + 4) * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
   unsigned char* As = smem;
   unsigned char* Bs = smem + 2 * HPIX * AROWB;
-  float* Ss = reinterpret_cast<float*>(Bs + 2 * BN * ROWB);
+  float* Ss = reinterpret_cast<float*>(Bs + 2 * BROWS * ROWB);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -641,7 +648,7 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
   const int n0 = n_tile * BN;
   const int ntl = prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0;
   const int nchunks = g.Ctot / CK;
-  const int csteps = nchunks * WINO_STEPS;
+  const int csteps = nchunks * STEPS;
 
   auto tile_xy = [&](int i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
     const unsigned pt = (unsigned)(prow + i * gp);
@@ -677,14 +684,15 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
     uint4 v[B_ROUNDS];
   };
   auto b_load = [&](int st) __attribute__((always_inline)) {  // st: step within a tile
-    const int chunk = st / WINO_STEPS, t = st - chunk * WINO_STEPS;
-    const int k0 = t * g.Ctot + chunk * CK;
+    const int chunk = st / STEPS, t = st - chunk * STEPS;
     BRegs rb;
 #pragma unroll
     for (int r = 0; r < B_ROUNDS; ++r) {
       const int idx = r * HTHREADS + tid;
       const int row = idx >> 3, cc = idx & 7;
-      rb.v[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + row) * k_pad + k0 + cc * E);
+      const int pl = row / BN, co = row - pl * BN;  // plane t*XS + pl, output column co
+      const int k0 = (t * XS + pl) * g.Ctot + chunk * CK;
+      rb.v[r] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + co) * k_pad + k0 + cc * E);
     }
     return rb;
   };
@@ -693,7 +701,7 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
     for (int r = 0; r < B_ROUNDS; ++r) {
       const int idx = r * HTHREADS + tid;
       const int row = idx >> 3, cc = idx & 7;
-      *reinterpret_cast<uint4*>(Bs + (buf * BN + row) * ROWB + cc * 16) = rb.v[r];
+      *reinterpret_cast<uint4*>(Bs + (buf * BROWS + row) * ROWB + cc * 16) = rb.v[r];
     }
   };
 
@@ -704,30 +712,53 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
     for (int b = 0; b < NT; ++b) acc[x][b] = f32x16{};
   const int prow0 = py * HWT + px2;  // LDS row of d_0 at dy = 0
 
-  // step t = (dy, xi): V_xi from two d_j rows of the halo, one MFMA pass per column subtile
+  // step t = (dy, xi) (XS = 1) or (dy, xi pair) (XS = 2): V_xi from d_j rows of the halo, one MFMA
+  // pass per plane and column subtile
   auto mma_step = [&](int hbuf, int bbuf, int t) __attribute__((always_inline)) {
     const unsigned char* a_src = As + hbuf * HPIX * AROWB;
-    const unsigned char* b_src = Bs + bbuf * BN * ROWB;
-    const int dy = t >> 2, xi = t & 3;
-    const int ja = xi == 0 ? 0 : (xi == 2 ? 2 : 1);
-    const int jb = xi == 3 ? 3 : (xi == 2 ? 1 : 2);
+    const unsigned char* b_src = Bs + bbuf * BROWS * ROWB;
+    const int dy = (t * XS) >> 2, x0i = (t * XS) & 3;
     const int sw = ((half ^ (py + dy)) & 1) * 16;
-    const unsigned char* pa = a_src + (prow0 + dy * HWT + (ja & 1) * (HWT / 2) + (ja >> 1)) * AROWB + sw;
-    const unsigned char* pb = a_src + (prow0 + dy * HWT + (jb & 1) * (HWT / 2) + (jb >> 1)) * AROWB + sw;
+    auto drow = [&](int j) { return a_src + (prow0 + dy * HWT + (j & 1) * (HWT / 2) + (j >> 1)) * AROWB + sw; };
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 da = *reinterpret_cast<const float4*>(pa + q * 32);
-      const float4 db = *reinterpret_cast<const float4*>(pb + q * 32);
-      uint4 bfr[NT];
+      uint4 bfr[XS][NT];
 #pragma unroll
-      for (int b = 0; b < NT; ++b)
-        bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * (BN / 2) + b * 32 + l32) * ROWB + q * 32 + half * 16);
-      float4 v;
-      if (xi == 1) v = make_float4(da.x + db.x, da.y + db.y, da.z + db.z, da.w + db.w);
-      else v = make_float4(da.x - db.x, da.y - db.y, da.z - db.z, da.w - db.w);
-      const uint4 av = make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
+      for (int p = 0; p < XS; ++p)
 #pragma unroll
-      for (int b = 0; b < NT; ++b) Mma<float>::run(acc[xi][b], av, bfr[b]);
+        for (int b = 0; b < NT; ++b)
+          bfr[p][b] = *reinterpret_cast<const uint4*>(b_src + (p * BN + wn * (BN / 2) + b * 32 + l32) * ROWB + q * 32 +
+                                                      half * 16);
+      float4 v[XS];
+      if (XS == 1) {
+        const int xi = x0i;
+        const int ja = xi == 0 ? 0 : (xi == 2 ? 2 : 1);
+        const int jb = xi == 3 ? 3 : (xi == 2 ? 1 : 2);
+        const float4 da = *reinterpret_cast<const float4*>(drow(ja) + q * 32);
+        const float4 db = *reinterpret_cast<const float4*>(drow(jb) + q * 32);
+        v[0] = xi == 1 ? make_float4(da.x + db.x, da.y + db.y, da.z + db.z, da.w + db.w)
+                       : make_float4(da.x - db.x, da.y - db.y, da.z - db.z, da.w - db.w);
+      } else {
+        // xi 0,1: d0 - d2, d1 + d2;  xi 2,3: d2 - d1, d1 - d3
+        const int j0 = x0i == 0 ? 0 : 1;
+        const float4 e0 = *reinterpret_cast<const float4*>(drow(j0) + q * 32);
+        const float4 e1 = *reinterpret_cast<const float4*>(drow(j0 + 1) + q * 32);
+        const float4 e2 = *reinterpret_cast<const float4*>(drow(j0 + 2) + q * 32);
+        if (x0i == 0) {
+          v[0] = make_float4(e0.x - e2.x, e0.y - e2.y, e0.z - e2.z, e0.w - e2.w);
+          v[XS - 1] = make_float4(e1.x + e2.x, e1.y + e2.y, e1.z + e2.z, e1.w + e2.w);
+        } else {
+          v[0] = make_float4(e1.x - e0.x, e1.y - e0.y, e1.z - e0.z, e1.w - e0.w);
+          v[XS - 1] = make_float4(e0.x - e2.x, e0.y - e2.y, e0.z - e2.z, e0.w - e2.w);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < XS; ++p) {
+        const uint4 av = make_uint4(__float_as_uint(v[p].x), __float_as_uint(v[p].y), __float_as_uint(v[p].z),
+                                    __float_as_uint(v[p].w));
+#pragma unroll
+        for (int b = 0; b < NT; ++b) Mma<float>::run(acc[x0i + p][b], av, bfr[p][b]);
+      }
     }
   };
   auto halo_put_global = [&](uint4 v, int r, const SrcArg& sa, int c, int y0, int x0, int hb)
@@ -785,26 +816,26 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
       float* ssh = Ss + 2 * CK + ((J + 1) & 1) * CK;
       float coef = 0.0f;
 #pragma unroll
-      for (int t = 0; t < WINO_STEPS; ++t) {
-        const int st2 = c * WINO_STEPS + t + 2;
+      for (int t = 0; t < STEPS; ++t) {
+        const int st2 = c * STEPS + t + 2;
         const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);
         if (t == 0 && !defer && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
 #pragma unroll
         for (int r = 0; r < A_ROUNDS; ++r) {
-          if (r == t) {
+          if (lt(r) == t) {
             int hp, cc;
             a_slot(r, hp, cc);
             ra[r] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
           }
         }
         mma_step(J & 1, S & 1, t);
-        if (defer && t == WINO_STEPS - 1) rb_hold = rb_next;
+        if (defer && t == STEPS - 1) rb_hold = rb_next;
         else b_store(rb_next, (S + 1) & 1);
         if (!defer) {
           if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
 #pragma unroll
           for (int r = 0; r < A_ROUNDS; ++r) {
-            if (r + 3 != t) continue;
+            if (lt(r) + 3 != t) continue;
             int hp, cc;
             if (a_slot(r, hp, cc)) {
               uint4 v = make_uint4(0, 0, 0, 0);
@@ -1322,6 +1353,285 @@ conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out,
   }
 }
 
+// fp32 weight gradient as the transpose of the Winograd F(2,3) forward (1-D along x). With
+// δ0, δ1 = dY at an output pair (x, x+1) and d_j = X at (x - 1 + j, row + dy):
+//   dW[dy][0] = M0 + (M1 + M2)/2,  dW[dy][1] = (M1 - M2)/2,  dW[dy][2] = (M1 + M2)/2 + M3,
+//   M_xi = sum over pairs of A_xi * B_xi,  A = (δ0, δ0 + δ1, δ0 - δ1, -δ1),
+//   B = (d0 - d2, d1 + d2, d2 - d1, d1 - d3)
+// (dW_i = dL/dg_i of the forward's Winograd form: the M_xi carry the G-transposed weights). The MFMA
+// k dimension is the output pair (two per k-step: one per lane half), so a 8x8 tile is 16 k-steps
+// of 4 products per dy instead of 32 of 3 taps: 2/3 of the direct kernel's MFMA work. Workgroup:
+// 64 co x 64 ci x the 12 (dy, xi) planes; 8 waves = 2 co halves x 2 ci halves x 2 plane groups
+// (planes 0-5 = dy 0 and dy 1 xi 0-1; 6-11 = dy 1 xi 2-3 and dy 2), 6 accumulators each. Each split
+// stores its M planes (plain stores, every plane has one owner) to ws[split][co][plane * C + ci]; the
+// fixed-order split reduction applies the output transform (wgrad_wino_reduce_kernel, gemm.hip).
+// Tiles are staged as in conv3x3_wgrad_halo_f32_kernel (double-buffered, next tile loaded during
+// the MFMAs, BN+ReLU of the producer applied at the LDS write).
+template <int TWW>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chunks, int64_t tiles_per_split,
+                              int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
+                              int ldw) {
+  constexpr int BI = 64, CJ = 64;
+  // pixel tile 8 x TWW (TWW = 16: 64 output pairs, 32 k-steps per tile, half the per-tile overhead of 8 x 8)
+  constexpr int WTH = FTH, WTW = TWW, WHW = TWW + 2, WPIXT = FTH * TWW, WHP = (FTH + 2) * (TWW + 2);
+  constexpr int NT = 512;
+  constexpr int P_ROUNDS = (WPIXT * BI / 4) / NT;
+  constexpr int X_ROUNDS = (WHP * (CJ / 4) + NT - 1) / NT;
+  constexpr int KS = WPIXT / 4;  // k-steps per tile: two pairs per k-step
+  constexpr int PPR = TWW / 2;   // pairs per tile row
+  static_assert(P_ROUNDS * NT == WPIXT * BI / 4, "dY tile must split evenly over the threads");
+
+  __shared__ __attribute__((aligned(16))) float Ps[2][WPIXT][BI];
+  __shared__ __attribute__((aligned(16))) float Xs[2][WHP][CJ];
+  __shared__ float Ks[2 * BI + 2 * CJ];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wj = wave & 1;          // ci half
+  const int wc = (wave >> 1) & 1;   // co half
+  const int tg = wave >> 2;         // plane group
+  const int half = lane >> 5, l32 = lane & 31;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int cot = lb % co_tiles;
+  const int rest = lb / co_tiles;
+  const int cik = rest % ci_chunks;
+  const int64_t split = rest / ci_chunks;
+  const int i0 = cot * BI;
+  const int c0 = cik * CJ;
+  const int64_t pt_begin = split * tiles_per_split;
+  const int64_t pt_end = min(total_tiles, pt_begin + tiles_per_split);
+
+  int xs_src = 0, xc = c0;
+  if (Q.nsrc > 1 && xc >= Q.src[0].C) {
+    xc -= Q.src[0].C;
+    xs_src = 1;
+  }
+  const SrcArg xa = pick_src(Q, xs_src);
+  const SrcArg& pa = P.src[0];
+  const int H = P.h, W = P.w;
+
+  if (tid < 2 * BI + 2 * CJ) {
+    float v;
+    if (tid < 2 * BI) {
+      const int c = i0 + (tid % BI);
+      v = pa.scale ? (tid < BI ? pa.scale[c] : pa.shift[c]) : 0.0f;
+    } else {
+      const int c = xc + ((tid - 2 * BI) % CJ);
+      v = xa.scale ? (tid < 2 * BI + CJ ? xa.scale[c] : xa.shift[c]) : 0.0f;
+    }
+    Ks[tid] = v;
+  }
+
+  auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
+    x0 = ((unsigned)pt - r2 * (unsigned)tiles_x) * WTW;
+    const unsigned r3 = r2 / (unsigned)tiles_y;
+    y0 = (r2 - r3 * (unsigned)tiles_y) * WTH;
+    img = (int)r3;
+  };
+  auto apply = [&](f32x4 v, const float* sc, const float* sh, int relu) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float f = v[j] * sc[j] + sh[j];
+      v[j] = relu ? fmaxf(f, 0.0f) : f;
+    }
+    return v;
+  };
+  f32x4 rp[P_ROUNDS], rx[X_ROUNDS];
+  auto load_p = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * NT + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      const int y = min(y0 + px / WTW, H - 1), x = min(x0 + px % WTW, W - 1);
+      rp[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pa.data) +
+                                              (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4);
+    }
+  };
+  auto load_x = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * NT + tid;
+      const int hp = min(idx >> 4, WHP - 1), cc = idx & 15;
+      const int y = min(max(y0 - 1 + hp / WHW, 0), H - 1), x = min(max(x0 - 1 + hp % WHW, 0), W - 1);
+      rx[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(xa.data) +
+                                              (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 4);
+    }
+  };
+  auto store_p = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * NT + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (y0 + px / WTW < H && x0 + px % WTW < W)
+        v = pa.scale ? apply(rp[r], Ks + cc * 4, Ks + BI + cc * 4, pa.relu) : rp[r];
+      *reinterpret_cast<f32x4*>(&Ps[buf][px][cc * 4]) = v;
+    }
+  };
+  auto store_x = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * NT + tid;
+      if (idx < WHP * (CJ / 4)) {
+        const int hp = idx >> 4, cc = idx & 15;
+        const int y = y0 - 1 + hp / WHW, x = x0 - 1 + hp % WHW;
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          v = xa.scale ? apply(rx[r], Ks + 2 * BI + cc * 4, Ks + 2 * BI + CJ + cc * 4, xa.relu) : rx[r];
+        *reinterpret_cast<f32x4*>(&Xs[buf][hp][cc * 4]) = v;
+      }
+    }
+  };
+
+  f32x16 acc[6];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) acc[t] = f32x16{};
+
+  // raw operands of one k-step: δ0, δ1 of the lane's pair and the seven d_j rows its planes use
+  // (group 0: dy 0 d0..d3, dy 1 d0..d2; group 1: dy 1 d1..d3, dy 2 d0..d3)
+  struct Frag {
+    float a0, a1, d[7];
+  };
+  const int dy_a = tg == 0 ? 0 : 1;   // row of the first four d (group 0: dy 0; group 1: dy 1 from j = 1)
+  auto frag = [&](int buf, int ks) __attribute__((always_inline)) {
+    Frag f;
+    const int pp = 2 * ks + half, r = pp / PPR, c2 = pp % PPR;
+    const float* pr = &Ps[buf][r * WTW + 2 * c2][wc * 32 + l32];
+    f.a0 = pr[0];
+    f.a1 = pr[BI];
+    const float* xr = &Xs[buf][r * WHW + 2 * c2][wj * 32 + l32];
+    if (tg == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f.d[j] = xr[j * CJ];            // dy 0
+#pragma unroll
+      for (int j = 0; j < 3; ++j) f.d[4 + j] = xr[(WHW + j) * CJ];  // dy 1, j = 0..2
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) f.d[j] = xr[(WHW + 1 + j) * CJ];  // dy 1, j = 1..3
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f.d[3 + j] = xr[(2 * WHW + j) * CJ];  // dy 2
+    }
+    return f;
+  };
+  (void)dy_a;
+  auto mma = [&](const Frag& f) __attribute__((always_inline)) {
+    const float A0 = f.a0, A1 = f.a0 + f.a1, A2 = f.a0 - f.a1, A3 = -f.a1;
+    if (tg == 0) {
+      const float* d = f.d;  // dy 0: d[0..3]; dy 1: d[4..6] = d0..d2
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[0] - d[2], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[1] + d[2], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[2] - d[1], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[1] - d[3], acc[3], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[4] - d[6], acc[4], 0, 0, 0);
+      acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[5] + d[6], acc[5], 0, 0, 0);
+    } else {
+      const float* d = f.d;  // dy 1: d[0..2] = d1..d3; dy 2: d[3..6] = d0..d3
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[1] - d[0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[0] - d[2], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[3] - d[5], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[4] + d[5], acc[3], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[5] - d[4], acc[4], 0, 0, 0);
+      acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[4] - d[6], acc[5], 0, 0, 0);
+    }
+  };
+
+  if (pt_begin < pt_end) {
+    load_p((int)pt_begin);
+    load_x((int)pt_begin);
+  }
+  __syncthreads();  // coefficients visible
+  if (pt_begin < pt_end) {
+    store_p((int)pt_begin, 0);
+    store_x((int)pt_begin, 0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+    const bool more = pt + 1 < (int)pt_end;
+    if (more) { load_p(pt + 1); load_x(pt + 1); }
+    Frag cur = frag(buf, 0);
+#pragma unroll 4
+    for (int ks = 0; ks < KS; ++ks) {
+      const Frag nxt = frag(buf, ks + 1 < KS ? ks + 1 : 0);
+      mma(cur);
+      cur = nxt;
+    }
+    if (more) { store_p(pt + 1, buf ^ 1); store_x(pt + 1, buf ^ 1); }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // planes of this wave: group 0 -> 0..5, group 1 -> 6..11 (plane = dy * 4 + xi)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const int ctot = Q.Ctot;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int plane = tg * 6 + t;
+    const int j = plane * ctot + c0 + wj * 32 + (ln & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = i0 + wc * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+      ws[split * ws_stride + (int64_t)i * ldw + j] = acc[t][r];
+    }
+  }
+}
+
+bool conv3x3_wgrad_wino_eligible(const GatherArg& p, const GatherArg& q, int dtype) {
+  static const bool on = [] {
+    const char* v = getenv("SELUNET_WINO_WGRAD");
+    return !(v && v[0] == '0');
+  }();
+  return on && dtype == SELUNET_F32 && conv3x3_wgrad_halo_eligible(p, q, dtype) && q.w % 2 == 0;
+}
+
+// splits of the Winograd weight gradient (64 x 64 tiles): ~256 workgroups over (co tile, ci chunk, split)
+static int wino_wgrad_tw() {
+  static const int tw = [] {
+    const char* v = getenv("SELUNET_WINO_WGRAD_TW");
+    return v && atoi(v) == 8 ? 8 : 16;
+  }();
+  return tw;
+}
+
+int64_t conv3x3_wgrad_wino_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
+  const int co_tiles = p.K / 64, ci_chunks = q.Ctot / 64;
+  const int64_t total = (int64_t)q.n * cdiv(q.w, wino_wgrad_tw()) * cdiv(q.h, FTH);
+  static const int64_t target = [] {
+    const char* e = getenv("SELUNET_WGRAD_WGS");
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
+  }();
+  const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
+  const int64_t per = cdiv(total, std::min(total, want));
+  if (per_out) *per_out = per;
+  return cdiv(total, per);
+}
+
+int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldw, hipStream_t st) {
+  const int co_tiles = p.K / 64, ci_chunks = q.Ctot / 64;
+  const int tw = wino_wgrad_tw();
+  const int tiles_x = (int)cdiv(q.w, tw), tiles_y = (int)cdiv(q.h, FTH);
+  const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
+  int64_t per;
+  const int64_t splits = conv3x3_wgrad_wino_splits(p, q, &per);
+  const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
+  auto kern = tw == 8 ? conv3x3_wgrad_wino_f32_kernel<8> : conv3x3_wgrad_wino_f32_kernel<16>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(512), 0, st, p, q, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
+                     ws, (int64_t)p.K * ldw, ldw);
+  return check_launch("conv3x3_wgrad_wino");
+}
+
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype) {
   if (dtype != SELUNET_BF16 && dtype != SELUNET_F32) return false;
   if (p.taps != 1 || p.nsrc != 1 || p.small || p.src[0].layout != 0 || p.K % 64 != 0) return false;
@@ -1469,12 +1779,12 @@ bool conv3x3_wino_eligible(const GatherArg& g, int N) {
          conv3x3_wino_shape_ok(g.h, g.w, g.Ctot, g.src[0].C, N);
 }
 
-template <int BN>
+template <int BN, int XS>
 static void launch_wino(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st) {
   const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
   const int n_tiles = N / BN;
   const int gp = persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
-  hipLaunchKernelGGL((conv3x3_wino_persist_kernel<BN>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, u,
+  hipLaunchKernelGGL((conv3x3_wino_persist_kernel<BN, XS>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, u,
                      N, WINO_STEPS * g.Ctot, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp);
 }
 
@@ -1483,8 +1793,8 @@ bool conv3x3_wino_bn128(int N, const EpiArg& ep) {
 }
 
 int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st) {
-  if (conv3x3_wino_bn128(N, ep)) launch_wino<128>(g, u, N, ep, st);
-  else launch_wino<64>(g, u, N, ep, st);
+  if (conv3x3_wino_bn128(N, ep)) launch_wino<128, 1>(g, u, N, ep, st);
+  else launch_wino<64, 2>(g, u, N, ep, st);
   return check_launch("conv3x3_wino");
 }
 

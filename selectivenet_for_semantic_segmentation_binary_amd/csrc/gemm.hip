@@ -850,6 +850,7 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
   GatherArg gq;
   const int vec = bf ? 8 : 4;
   if (make_gather(a, dtype, g, vec) || make_gather(q, dtype, gq, vec)) return "invalid";
+  if (halo_enabled() && conv3x3_wgrad_wino_eligible(g, gq, dtype)) return "conv3x3_wgrad_wino_f32<64>";
   if (halo_enabled() && conv3x3_wgrad_halo_eligible(g, gq, dtype)) {
     if (bf) return g.K % 128 == 0 ? "conv3x3_wgrad_halo<128>" : "conv3x3_wgrad_halo<64>";
     return g.K % 128 == 0 ? "conv3x3_wgrad_halo_f32<128>" : "conv3x3_wgrad_halo_f32<64>";
@@ -985,10 +986,60 @@ __global__ void __launch_bounds__(64) wgrad_reduce_kernel(const float* __restric
   }
 }
 
+// Fixed-order split reduction of the fp32 Winograd weight gradient's M planes
+// (conv3x3_wgrad_wino_f32_kernel: ws[split][co][(dy*4 + xi)*C + c]) with the output transform
+// dW[dy][0] = M0 + (M1+M2)/2, dW[dy][1] = (M1-M2)/2, dW[dy][2] = (M1+M2)/2 + M3, written as the
+// packed [co][ldo] (column tap*C + c) or the Conv2d [co][C][3][3] layout. One lane per (co, dy, 4 c).
+template <int LAYOUT>
+__global__ void __launch_bounds__(64) wgrad_wino_reduce_kernel(const float* __restrict__ ws, int64_t splits,
+                                                               int64_t stride, int ni, int ctot, int ldo,
+                                                               float* __restrict__ out) {
+  const int c4n = ctot / 4;
+  const int64_t n = (int64_t)ni * 3 * c4n;
+  const int ldw = 12 * ctot;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(v % c4n) * 4;
+    const int64_t r2 = v / c4n;
+    const int dy = (int)(r2 % 3);
+    const int64_t row = r2 / 3;
+    const float* base = ws + row * ldw + dy * 4 * ctot + c;
+    f32x4 m[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    constexpr int U = 4;
+    int64_t sp = 0;
+    for (; sp + U <= splits; sp += U) {
+      f32x4 x[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[u][k] = *reinterpret_cast<const f32x4*>(base + (sp + u) * stride + k * ctot);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] += x[u][k];
+    }
+    for (; sp < splits; ++sp)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m[k] += *reinterpret_cast<const f32x4*>(base + sp * stride + k * ctot);
+    const f32x4 s12 = (m[1] + m[2]) * 0.5f;
+    const f32x4 t[3] = {m[0] + s12, (m[1] - m[2]) * 0.5f, s12 + m[3]};
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int tap = dy * 3 + dx;
+      if constexpr (LAYOUT == WG_PACKED) {
+        *reinterpret_cast<f32x4*>(out + row * ldo + tap * ctot + c) = t[dx];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) out[(row * ctot + c + u) * 9 + tap] = t[dx][u];
+      }
+    }
+  }
+}
+
 struct WgradPlan {
   GatherArg gp, gq;
   int ni, bj, nj_pad;
   bool halo;
+  bool wino;       // fp32 Winograd planes (split-partials paths only): ws row length 12 * C
   int64_t splits;  // pixel splits whose partials the fixed-order reduction sums
 };
 
@@ -1004,13 +1055,32 @@ static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t 
   w.bj = (w.gq.K % 128 == 0 || w.gq.K > 512) ? 128 : 64;
   w.nj_pad = (int)(cdiv(w.gq.K, w.bj) * w.bj);
   w.halo = halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, dtype);
-  if (w.halo) {
+  w.wino = w.halo && conv3x3_wgrad_wino_eligible(w.gp, w.gq, dtype);
+  if (w.wino) {
+    w.splits = conv3x3_wgrad_wino_splits(w.gp, w.gq, nullptr);
+  } else if (w.halo) {
     w.splits = conv3x3_wgrad_halo_splits(w.gp, w.gq, dtype, nullptr);
   } else {
     const int bi = w.ni % 128 == 0 ? 128 : 64;
     w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
   }
   return 0;
+}
+
+// workspace floats per split: [ni][nj_pad], or [ni][12 C] for the Winograd planes
+static int64_t wgrad_ws_row(const WgradPlan& w) { return w.wino ? 12 * (int64_t)w.gq.Ctot : (int64_t)w.nj_pad; }
+
+// Winograd planes -> the split reduction with the output transform (layout WG_PACKED: out [ni][nj_pad])
+static void launch_wino_reduce(const WgradPlan& w, float* ws, int layout, float* out, hipStream_t st) {
+  const int64_t n = (int64_t)w.ni * 3 * (w.gq.Ctot / 4);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 64), 16384));
+  const int64_t stride = (int64_t)w.ni * wgrad_ws_row(w);
+  if (layout == WG_CONV3X3)
+    hipLaunchKernelGGL(wgrad_wino_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits, stride, w.ni,
+                       w.gq.Ctot, w.nj_pad, out);
+  else
+    hipLaunchKernelGGL(wgrad_wino_reduce_kernel<WG_PACKED>, dim3(blocks), dim3(64), 0, st, ws, w.splits, stride, w.ni,
+                       w.gq.Ctot, w.nj_pad, out);
 }
 
 static void launch_wgrad_any(const WgradPlan& w, float* out, float* ws, int32_t dtype, hipStream_t st) {
@@ -1040,6 +1110,7 @@ extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather*
   WgradPlan w;
   if (int rc = plan_wgrad(p, q, dtype, w)) return rc;
   SELUNET_REQUIRE(out != nullptr, "out is NULL");
+  w.wino = false;  // atomics into the packed output: the direct kernels
   launch_wgrad_any(w, out, nullptr, dtype, as_stream(stream));
   return check_launch("gemm_wgrad");
 }
@@ -1047,7 +1118,7 @@ extern "C" int selunet_gemm_wgrad(const selunet_gather* p, const selunet_gather*
 extern "C" int64_t selunet_gemm_wgrad_ws_bytes(const selunet_gather* p, const selunet_gather* q, int32_t dtype) {
   WgradPlan w;
   if (plan_wgrad(p, q, dtype, w)) return -1;
-  return w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  return w.splits * (int64_t)w.ni * wgrad_ws_row(w) * 4;
 }
 
 extern "C" int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gather* q, float* out, float* ws,
@@ -1055,8 +1126,16 @@ extern "C" int selunet_gemm_wgrad_ws(const selunet_gather* p, const selunet_gath
   WgradPlan w;
   if (int rc = plan_wgrad(p, q, dtype, w)) return rc;
   SELUNET_REQUIRE(out != nullptr, "out is NULL");
-  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  const int64_t need = w.splits * (int64_t)w.ni * wgrad_ws_row(w) * 4;
   hipStream_t st = as_stream(stream);
+  if (w.wino) {
+    SELUNET_REQUIRE(ws != nullptr && ws_bytes >= need, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                    (long long)ws_bytes);
+    if (int rc = conv3x3_wgrad_wino_launch(w.gp, w.gq, ws, 12 * w.gq.Ctot, st)) return rc;
+    SELUNET_REQUIRE(hipMemsetAsync(out, 0, (size_t)w.ni * w.nj_pad * 4, st) == hipSuccess, "hipMemsetAsync failed");
+    launch_wino_reduce(w, ws, WG_PACKED, out, st);
+    return check_launch("gemm_wgrad_ws");
+  }
   if (need == 0) {  // no split-partials path for these operands: zero + atomics
     SELUNET_REQUIRE(hipMemsetAsync(out, 0, (size_t)w.ni * w.nj_pad * 4, st) == hipSuccess, "hipMemsetAsync failed");
     launch_wgrad_any(w, out, nullptr, dtype, st);
@@ -1082,7 +1161,16 @@ extern "C" int selunet_gemm_wgrad_ws_to(const selunet_gather* p, const selunet_g
   SELUNET_REQUIRE(out != nullptr && (layout == WG_CONV3X3 || layout == WG_CONVT), "wgrad_ws_to: bad arguments");
   SELUNET_REQUIRE(w.gq.K % (layout == WG_CONV3X3 ? 9 : 4) == 0, "wgrad_ws_to: K_q = %d is not a multiple of %d",
                   w.gq.K, layout == WG_CONV3X3 ? 9 : 4);
-  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  const int64_t need = w.splits * (int64_t)w.ni * wgrad_ws_row(w) * 4;
+  if (w.wino) {
+    SELUNET_REQUIRE(layout == WG_CONV3X3, "wgrad_ws_to: the Winograd planes are a 3x3 weight gradient");
+    SELUNET_REQUIRE(ws != nullptr && ws_bytes >= need, "workspace of %lld bytes needed (got %lld)", (long long)need,
+                    (long long)ws_bytes);
+    hipStream_t st = as_stream(stream);
+    if (int rc = conv3x3_wgrad_wino_launch(w.gp, w.gq, ws, 12 * w.gq.Ctot, st)) return rc;
+    launch_wino_reduce(w, ws, WG_CONV3X3, out, st);
+    return check_launch("gemm_wgrad_ws_to");
+  }
   if (need == 0) {
     SELUNET_REQUIRE(packed != nullptr, "wgrad_ws_to: packed scratch is NULL");
     if (int rc = selunet_gemm_wgrad_ws(p, q, packed, ws, ws_bytes, dtype, stream)) return rc;

@@ -409,6 +409,9 @@ int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, con
                         hipStream_t st);
 // fp32 1-D Winograd F(2,3) forward / data gradient (conv3x3.hip, selunet_conv3x3_wino)
 bool conv3x3_wino_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
+bool conv3x3_wgrad_wino_eligible(const GatherArg& p, const GatherArg& q, int dtype);
+int64_t conv3x3_wgrad_wino_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
+int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldw, hipStream_t st);
 bool conv3x3_wino_eligible(const GatherArg& g, int N);
 bool conv3x3_wino_bn128(int N, const EpiArg& ep);
 int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st);

@@ -147,3 +147,45 @@ def test_wino_rejects_ineligible():
     ep = K.Epilogue(K.ptr(y), None, None, None, K.EP_PLAIN, 0)
     with pytest.raises(K.SelunetError):
         K.call("selunet_conv3x3_wino", K.gather(n, h, w, 9, K.source(x, c)), K.ptr(u), 64, ep, K.stream_ptr())
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,xform,n,h,w", [
+    (64, 0, 64, True, 2, 16, 16),
+    (64, 64, 128, True, 2, 16, 16),     # two sources (torch.cat), BN+ReLU staging
+    (128, 0, 256, False, 1, 20, 36),    # ragged 8x8 tiles in both directions
+    (256, 0, 64, True, 3, 12, 18),      # ragged rows, odd tile counts
+])
+def test_wino_wgrad(cin0, cin1, cout, xform, n, h, w):
+    """fp32 Winograd weight gradient (conv3x3_wgrad_wino_f32_kernel + the plane reduction) through
+    selunet_gemm_wgrad_ws_to (the Conv2d weight layout) and selunet_gemm_wgrad_ws (packed), against
+    torch's conv2d weight gradient in fp64; the two entry points agree bit for bit."""
+    x0 = gen(n, cin0, h, w, seed=9)
+    s0, t0 = bn_fold(cin0, 20)
+    a = torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)) if xform else x0
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    keep = [d(nhwc(x0)), d(s0), d(t0)]
+    srcs = [K.source(keep[0], cin0, keep[1] if xform else None, keep[2] if xform else None)]
+    if cin1:
+        x1 = gen(n, cin1, h, w, seed=10)
+        s1, t1 = bn_fold(cin1, 22)
+        a = torch.cat((a, torch.relu(x1 * s1.view(1, -1, 1, 1) + t1.view(1, -1, 1, 1))), 1)
+        keep += [d(nhwc(x1)), d(s1), d(t1)]
+        srcs.append(K.source(keep[3], cin1, keep[4], keep[5]))
+    cin = cin0 + cin1
+    wt = gen(cout, cin, 3, 3, seed=11, scale=0.05).double().requires_grad_()
+    dy = gen(n, cout, h, w, seed=12)
+    (ref,) = torch.autograd.grad(F.conv2d(a.double(), wt, padding=1), wt, dy.double())
+    dyd = d(nhwc(dy))
+    gp, gq = K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs)
+    assert K.query("selunet_gemm_kernel_name", gp, gq, 0, 0, K.F32).decode() == "conv3x3_wgrad_wino_f32<64>"
+    wsb = K.query("selunet_gemm_wgrad_ws_bytes", gp, gq, K.F32)
+    ws = torch.empty(wsb // 4, device=DEV)
+    out = torch.full((cout, cin, 3, 3), float("nan"), device=DEV)
+    K.call("selunet_gemm_wgrad_ws_to", gp, gq, None, K.ptr(ws), wsb, K.WG_CONV3X3, K.ptr(out), K.F32, K.stream_ptr())
+    ld = K.query("selunet_wgrad_ld", 9 * cin)
+    packed = torch.full((cout, ld), float("nan"), device=DEV)
+    K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, K.F32, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel(out.cpu(), ref) < TOL
+    unpacked = packed[:, :9 * cin].reshape(cout, 9, cin).permute(0, 2, 1).reshape(cout, cin, 3, 3)
+    assert torch.equal(unpacked, out) and torch.all(packed[:, 9 * cin:] == 0)

@@ -5,5 +5,5 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 for lib in $R/_ab/libselunet_*.so; do
   echo "== $(basename $lib)"
   SELUNET_LIB=$lib timeout -k 5 120 python3 $R/tools/conv_bench.py --dtype ${DTYPE:-fp32} --only ${ONLY:-fwd} \
-    --iters 5 --layers ${LAYERS:-enc1_2,dec1_2,enc2_2,dec3_1} || exit $?
+    --iters 5 --layers ${LAYERS:-enc1_2,dec1_2,enc2_2,dec3_1} ${EXTRA:-} || exit $?
 done

@@ -44,6 +44,8 @@ for _t in ("bf16", "f32"):
         (_pat("first_conv_wgrad_kernel", _t), f"first_conv_wgrad<{_t}>"),
     ]
 NAME_MAP += [
+    (_pat("conv3x3_wino_persist_kernel", 128), "conv3x3_wino<f32,128>"),
+    (_pat("conv3x3_wino_persist_kernel", 64), "conv3x3_wino<f32,64>"),
     (_pat("conv3x3_wgrad_halo_f32_kernel", 128), "conv3x3_wgrad_halo_f32<128>"),
     (_pat("conv3x3_wgrad_halo_f32_kernel", 64), "conv3x3_wgrad_halo_f32<64>"),
     (_pat("conv3x3_wgrad_halo_kernel", 128), "conv3x3_wgrad_halo<128>"),
