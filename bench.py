@@ -130,6 +130,8 @@ class KernelTimer:
             if name != "selunet_gemm_wgrad" and _i(args[4]) > 0:
                 kname += "+reduce"  # (the entry point's time includes the split reduction)
             flops = 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
+            if "wino" in kname:  # Winograd F(2,3) transpose: 4 products per output pair and row, not 6
+                flops *= 2.0 / 3.0
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             return kname, "mfma", flops, nbytes, f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
         if name == "selunet_first_conv_fwd":  # (x, n, cin, h, w, wpack, y, stats, dtype, stream)

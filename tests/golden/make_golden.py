@@ -377,7 +377,7 @@ def kats():
     print(f"wrote {path}: bce={bce:.4f} ce={ce:.4f} miou={data['miou']:.6f} thr={train_thr!r},{eval_thr!r}")
 
 
-def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0):
+def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0, member=0):
     """mIoU parity run (BASELINE.json 'mIoU parity'): the reference training loop
     (train.py:183-241: forward, BCEWithLogits aux + calc_selective_risk_image_b, Adam, the
     per-batch Evaluator on the fp64-sigmoid masks) for `epochs` passes over a seeded synthetic
@@ -390,6 +390,8 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
     vi, vl = make_patches(n_val, size, seed=2025)
     xtr, ltr = preprocess(ti, tl)
     xva, lva = preprocess(vi, vl)
+    if member:  # ensemble member: the training inputs perturbed at the rounding level (_perturbed)
+        xtr = _perturbed(xtr, member)
     torch.manual_seed(0)
     net = build_ref(seed, True)
     optim = torch.optim.Adam(net.parameters(), lr=1e-3)
@@ -436,6 +438,8 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
     out.update({"val_losses": np.array(vlosses), "val_cm_selective": evs.confusion_matrix.copy(),
                 "val_cm": evp.confusion_matrix.copy(), "val_miou_selective": np.float64(evs.get_mIoU()),
                 "val_miou": np.float64(evp.get_mIoU()), "val_selected": np.int64(vsel)})
+    if member:
+        return out
     path = os.path.join(HERE, fname)
     np.savez_compressed(path, **out)
     print(f"wrote {path}: train loss {losses[0]:.4f} -> {losses[-1]:.4f}, val mIoU {out['val_miou']:.4f} "
@@ -526,6 +530,95 @@ def _sampled(d, name, g):
     if f"s0/gradfull/{name}" in d:
         return a
     return a[d[f"s0/gradidx/{name}"]]
+
+
+def miou_spread(k_members=8, fname="miou_sel_64.npz"):
+    """How far apart do two fp32 runs of the reference's own training land? Re-run the mIoU
+    fixture's training (miou_fixture) on K copies of the training inputs perturbed at the rounding
+    level and record their validation / training mIoU next to the unperturbed run's
+    (`*_miou_ens`): 40 Adam steps amplify rounding noise through ReLU/max-pool kinks exactly as one
+    step does for the gradients (augment_ensemble)."""
+    path = os.path.join(HERE, fname)
+    d = dict(np.load(path, allow_pickle=False))
+    runs = []
+    for k in range(1, k_members + 1):
+        r = miou_fixture(member=k)
+        m_tr = _miou_cm(r["train_cm"])
+        runs.append((float(r["val_miou"]), float(r["val_miou_selective"]), m_tr))
+        print(f"member {k}: val mIoU {runs[-1][0]:.5f} selective {runs[-1][1]:.5f} train {m_tr:.5f} "
+              f"(unperturbed {float(d['val_miou']):.5f} / {float(d['val_miou_selective']):.5f})", flush=True)
+    d["val_miou_ens"] = np.array([r[0] for r in runs])
+    d["val_miou_selective_ens"] = np.array([r[1] for r in runs])
+    d["train_miou_ens"] = np.array([r[2] for r in runs])
+    np.savez_compressed(path, **d)
+    print(f"wrote {path}: {k_members}-member spread of the reference's mIoU")
+
+
+def _miou_cm(cm):
+    cm = np.asarray(cm, dtype=np.float64)
+    iou = np.diag(cm) / (cm.sum(0) + cm.sum(1) - np.diag(cm))
+    return float(np.nanmean(iou))
+
+
+def _conv_noise_hooks(net, eps, member):
+    """Forward hooks that multiply every Conv2d / ConvTranspose2d output of the reference by
+    (1 + eps * N(0, 1)) elementwise (member-seeded): the per-output rounding difference between two
+    valid fp32 convolution implementations (summation order, algorithm), injected where an
+    implementation's own rounding enters — at every layer, not only at the input."""
+    gen = torch.Generator().manual_seed(5000 + member)
+    hooks = []
+    for m in net.modules():
+        if isinstance(m, (torch.nn.Conv2d, torch.nn.ConvTranspose2d)):
+            def hook(mod, inp, out):
+                z = torch.randn(out.shape, generator=gen, dtype=torch.float64).to(out.dtype)
+                return out + out * (eps * z)  # (not out * (1 + eps z): 1 + 2e-7 z rounds in fp32)
+            hooks.append(m.register_forward_hook(hook))
+    return hooks
+
+
+def augment_conv_noise(fname, k_members=8, eps=2e-7):
+    """Second ensemble for fixtures with an fp64 truth: the reference's fp32 step with
+    rounding-level noise on every convolution output (_conv_noise_hooks), each member's error
+    against the unperturbed fp64 truth -> `s0/grad_ens_conv/<name>` (largest over members). eps =
+    2e-7: the measured RMS relative difference between two direct fp32 summations of one conv
+    output (1.6-1.8e-7 each against fp64, tools/wino_error.py)."""
+    path = os.path.join(HERE, fname)
+    d = dict(np.load(path, allow_pickle=False))
+    n, size = int(d["meta_n"]), int(d["meta_size"])
+    selective, lamb = bool(d["meta_selective"]), int(d["meta_lamb"])
+    chunks, seed = int(d.get("meta_chunks", 1)), int(d["meta_seed"])
+    x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
+    ce = "meta_n_cls" in d
+    if ce:
+        lab = lab.astype(np.int64)
+    names = [k[len("s0/gradnorm/"):] for k in d if k.startswith("s0/gradnorm/")]
+    assert all(f"s0/grad64norm/{nm}" in d for nm in names), "needs the fp64 truth"
+    worst = {nm: 0.0 for nm in names}
+    for k in range(1, k_members + 1):
+        if ce:
+            net = build_ref_ce(seed, selective, int(d["meta_n_cls"])).train()
+            hooks = _conv_noise_hooks(net, eps, k)
+            optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+            r = ref_step_ce(net, optim, torch.tensor(x), torch.tensor(lab), selective, lamb)
+        else:
+            net = build_ref(seed, selective).train()
+            hooks = _conv_noise_hooks(net, eps, k)
+            optim = torch.optim.Adam(net.parameters(), lr=1e-3)
+            r = ref_step(net, optim, torch.tensor(x), torch.tensor(lab), selective, lamb, chunks)
+        for h in hooks:
+            h.remove()
+        for nm, g in r["grads"].items():
+            g32 = _sampled(d, nm, g)
+            ref = (d[f"s0/grad64full/{nm}"] if f"s0/grad64full/{nm}" in d else d[f"s0/grad64val/{nm}"]).astype(np.float64)
+            worst[nm] = max(worst[nm], float(np.linalg.norm(g32 - ref) / max(np.linalg.norm(ref), 1e-30)))
+        del net, optim, r
+        print(f"{fname}: conv-noise member {k}/{k_members} done", flush=True)
+    for nm, e in worst.items():
+        d["s0/grad_ens_conv/" + nm] = np.float64(e)
+    d["meta_ens_conv_members"] = np.int64(k_members)
+    d["meta_ens_conv_eps"] = np.float64(eps)
+    np.savez_compressed(path, **d)
+    print(f"wrote {path} with the {k_members}-member conv-output noise ensemble (eps {eps:g})")
 
 
 def augment_ensemble(fname, k_members=8, ckpt=False):
@@ -643,6 +736,13 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["miou"]:
         miou_fixture()
+        sys.exit(0)
+    if sys.argv[1:2] == ["conv_noise"]:
+        for f in sys.argv[2:]:
+            augment_conv_noise(f, k_members=int(os.environ.get("ENS_MEMBERS", 16)))
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou_spread"]:
+        miou_spread(int(sys.argv[2]) if len(sys.argv) > 2 else 8)
         sys.exit(0)
     if sys.argv[1:] == ["ce"]:
         ce_step_fixture("step_ce_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)

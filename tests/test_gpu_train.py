@@ -116,8 +116,14 @@ def test_miou_parity_vs_reference_training(dtype, tol):
     m_sel, m_all = mean_iou(vs.confusion_matrix()), mean_iou(vp.confusion_matrix())
     print(f"val mIoU {m_all:.5f} (reference {float(d['val_miou']):.5f}), selective {m_sel:.5f} "
           f"(reference {float(d['val_miou_selective']):.5f})")
-    assert abs(m_all - float(d["val_miou"])) <= tol
-    assert abs(m_sel - float(d["val_miou_selective"])) <= tol
+    # The validation mIoU after 40 Adam steps is chaotic: the reference's own fp32 run moves by up
+    # to 0.0079 when its training inputs are perturbed by 1e-7 relative (8 members,
+    # make_golden.py::miou_spread; the training-phase mIoU above moves by 2e-4). The bound is
+    # tol or that spread, whichever is larger.
+    for got, key in ((m_all, "val_miou"), (m_sel, "val_miou_selective")):
+        ens = d[key + "_ens"] if key + "_ens" in d.files else np.zeros(1)
+        spread = float(np.abs(ens - float(d[key])).max())
+        assert abs(got - float(d[key])) <= max(tol, spread), (key, got, float(d[key]), spread)
 
 
 def _cli(tmp, *extra):

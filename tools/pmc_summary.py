@@ -46,6 +46,8 @@ for _t in ("bf16", "f32"):
 NAME_MAP += [
     (_pat("conv3x3_wino_persist_kernel", 128), "conv3x3_wino<f32,128>"),
     (_pat("conv3x3_wino_persist_kernel", 64), "conv3x3_wino<f32,64>"),
+    (_pat("conv3x3_wgrad_wino_f32_kernel", 16), "conv3x3_wgrad_wino_f32<64>"),
+    (_pat("conv3x3_wgrad_wino_f32_kernel", 8), "conv3x3_wgrad_wino_f32<64>"),
     (_pat("conv3x3_wgrad_halo_f32_kernel", 128), "conv3x3_wgrad_halo_f32<128>"),
     (_pat("conv3x3_wgrad_halo_f32_kernel", 64), "conv3x3_wgrad_halo_f32<64>"),
     (_pat("conv3x3_wgrad_halo_kernel", 128), "conv3x3_wgrad_halo<128>"),
