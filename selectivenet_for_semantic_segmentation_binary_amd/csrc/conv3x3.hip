@@ -791,7 +791,13 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
   rb_next = b_load(1 % csteps);
   __syncthreads();
 
-  using Acc = typename StatAcc<T>::type;
+  // Statistics registers: fp64 as in the direct kernel at BN = 64; at BN = 128 the 48 registers of fp64
+  // sums (8 columns x 3 sets) push the kernel past 256 VGPRs (39 spills: +240 MB of scratch writes per
+  // launch, PMC) — there they are fp32 (4.5% faster, tools/ab_conv.sh). The per-tile partials are
+  // fp32 either way; the fp32 sum over a workgroup's ~128 tiles adds ~sqrt(128) ulp to BN-backward
+  // and bias sums that the fp64 slab reduction then combines; the forward's first-pass mean only
+  // centres the second, exact pass (selunet_bn_centered_partials).
+  using Acc = std::conditional_t<BN == 128, float, typename StatAcc<T>::type>;
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const TileStats ts = tile_stats(ep, prow, n0, N);

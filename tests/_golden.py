@@ -63,8 +63,8 @@ def grad_bound(e_ref, e_ens=0.0):
     e_ref: the reference fp32 run's error on the same samples; e_ens: the largest error of the
     reference's fp32 runs under rounding-level perturbations — of the input (`s0/grad_ens/<name>`,
     tests/golden/make_golden.py::augment_ensemble) and, where the fixture has it, of every
-    convolution output (2e-7 relative, the difference between two fp32 summation orders of one
-    output: `s0/grad_ens_conv/<name>`, augment_conv_noise), whichever is larger. ReLU-mask / max-pool-argmax flips make the fp32
+    convolution output (3e-7 relative, the measured rounding of the fp32 Winograd F(2,3)
+    convolution: `s0/grad_ens_conv/<name>`, augment_conv_noise), whichever is larger. ReLU-mask / max-pool-argmax flips make the fp32
     gradient a discontinuous function of rounding noise, so one reference run's error is one draw:
     the same 1e-7 input perturbation moves the reference's own error on a tensor from 1e-6 to 1e-3
     (DESIGN.md §4). Bound: max(1e-4, 10 e_ref, 3 e_ens) — for a tensor no perturbation disturbs

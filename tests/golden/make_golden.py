@@ -562,9 +562,9 @@ def _miou_cm(cm):
 
 def _conv_noise_hooks(net, eps, member):
     """Forward hooks that multiply every Conv2d / ConvTranspose2d output of the reference by
-    (1 + eps * N(0, 1)) elementwise (member-seeded): the per-output rounding difference between two
-    valid fp32 convolution implementations (summation order, algorithm), injected where an
-    implementation's own rounding enters — at every layer, not only at the input."""
+    (1 + eps * N(0, 1)) elementwise (member-seeded): the per-output rounding of an fp32 convolution
+    algorithm (summation order, Winograd transforms), injected where an implementation's own
+    rounding enters — at every layer, not only at the input."""
     gen = torch.Generator().manual_seed(5000 + member)
     hooks = []
     for m in net.modules():
@@ -576,12 +576,13 @@ def _conv_noise_hooks(net, eps, member):
     return hooks
 
 
-def augment_conv_noise(fname, k_members=8, eps=2e-7):
+def augment_conv_noise(fname, k_members=8, eps=3e-7):
     """Second ensemble for fixtures with an fp64 truth: the reference's fp32 step with
     rounding-level noise on every convolution output (_conv_noise_hooks), each member's error
     against the unperturbed fp64 truth -> `s0/grad_ens_conv/<name>` (largest over members). eps =
-    2e-7: the measured RMS relative difference between two direct fp32 summations of one conv
-    output (1.6-1.8e-7 each against fp64, tools/wino_error.py)."""
+    3e-7: the measured RMS relative error against fp64 of one fp32 convolution output computed as
+    the 1-D Winograd F(2,3) the fp32 kernels use (3.1e-7 at C = 256/512; a direct fp32 sum:
+    1.6-1.8e-7; tools/wino_error.py)."""
     path = os.path.join(HERE, fname)
     d = dict(np.load(path, allow_pickle=False))
     n, size = int(d["meta_n"]), int(d["meta_size"])

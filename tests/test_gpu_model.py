@@ -235,6 +235,32 @@ def test_adam_matches_reference_algorithm():
     ropt2.load_state_dict(sd)  # checkpoint interchangeability (utils/net_utils.py:5-9)
 
 
+class _conv_noise:
+    """Context: the oracle module's conv2d / conv_transpose2d outputs get out + out * eps * N(0, 1)
+    (member-seeded) — the conv-output noise ensemble of tests/golden/make_golden.py."""
+
+    def __init__(self, mod, eps, member):
+        self.mod, self.eps, self.gen = mod, eps, torch.Generator().manual_seed(5000 + member)
+
+    def _wrap(self, fn):
+        def f(*a, **kw):
+            out = fn(*a, **kw)
+            z = torch.randn(out.shape, generator=self.gen, dtype=torch.float64).to(out.dtype)
+            return out + out * (self.eps * z)
+        return f
+
+    def __enter__(self):
+        import types
+        self.F = self.mod.F
+        ns = types.SimpleNamespace(**{k: getattr(self.F, k) for k in dir(self.F) if not k.startswith("__")})
+        ns.conv2d, ns.conv_transpose2d = self._wrap(self.F.conv2d), self._wrap(self.F.conv_transpose2d)
+        self.mod.F = ns
+        return self
+
+    def __exit__(self, *exc):
+        self.mod.F = self.F
+
+
 @pytest.mark.parametrize("input_type,n,h,w,selective", [
     ("GH", 2, 32, 32, True),     # model.py:24-27: 'GH' inputs have 2 channels
     ("RGB", 1, 32, 48, True),    # batch of one, non-square patches
@@ -294,6 +320,16 @@ def test_step_against_oracle_shapes(input_type, n, h, w, selective):
         _, p64 = oracle(torch.float64, xp)
         for k in p64:
             ens[k] = max(ens.get(k, 0.0), float((p32[k] - p64[k]).norm() / (p64[k].norm() + 1e-30)))
+    # ... and with rounding-level noise on every convolution output (3e-7 relative: the measured
+    # rounding of the fp32 Winograd F(2,3) convolution against fp64; make_golden.py::
+    # augment_conv_noise), against the unperturbed fp64 run. At 3x48x32 (non-selective) one ReLU
+    # input of encoder_layer_2_x sits within that noise of zero: 2 of 16 oracle members flip it and
+    # land at 7.36e-4 on encoder_layer_2_1.0.weight — as does the HIP path; none flips at 2e-7.
+    for m in range(1, 9):
+        with _conv_noise(O, 3e-7, m):
+            _, p32 = oracle(torch.float32)
+        for k in g64:
+            ens[k] = max(ens[k], float((p32[k] - g64[k]).norm() / (g64[k].norm() + 1e-30)))
     for k, q in net.named_parameters():
         if k in PRE_BN_BIAS:  # cancels inside training-mode BN: zero gradient on both sides
             continue
