@@ -1066,49 +1066,57 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
   __syncthreads();  // coefficients visible
   store_tile((int)pt_begin, 0);
   __syncthreads();
-  int buf = 0;
-  for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
-    const bool more = pt + 1 < (int)pt_end;
-    load_tile(more ? pt + 1 : pt);
-    __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
-#pragma unroll
-    for (int ks = 0; ks < WTH; ++ks) {   // one tile row (16 pixels) per k-step
-      const int prow = ks * WTW + 8 * half + q4;
-      const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow][pcol]);
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow + 4][pcol]);
-      const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      const int xcol = wj * 32 + 16 * grp_hi + 4 * p4;
-      // tap fragments are read PF taps ahead of their MFMA (a rolling window of PF+1 fragments:
-      // hoisting all nine would spill), pinned in that order with sched_group_barrier so the LDS
-      // latency hides behind the MFMAs already issued instead of being waited out per MFMA
-      constexpr int PF = 3;
-      auto read_tap = [&](int t) __attribute__((always_inline)) {
-        const int tap = min(tap0 + t, 8);
-        const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-        const int xrow = (ks + dy) * WHW + 8 * half + dx + q4;
-        s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow][xcol]);
-        s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow + 4][xcol]);
-        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
-      };
-      bf16x8 bfr[NTAP];
-#pragma unroll
-      for (int t = 0; t < PF && t < NTAP; ++t) bfr[t] = read_tap(t);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * PF, 0);
-#pragma unroll
-      for (int t = 0; t < NTAP; ++t) {
-        if (t < ntap) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[t], acc[t], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (t + PF < NTAP) {
-          bfr[t + PF] = read_tap(t + PF);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+  // the tap count is a template constant of the tile loop: a per-k-step branch on the wave's (runtime)
+  // tap group would split the scheduled MFMA/read groups into blocks joined by LDS-counter drains
+  auto tile_loop = [&](auto ntc) __attribute__((always_inline)) {
+    constexpr int NTP = decltype(ntc)::value;
+    int buf = 0;
+    for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+      const bool more = pt + 1 < (int)pt_end;
+      load_tile(more ? pt + 1 : pt);
+      __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
+  #pragma unroll
+      for (int ks = 0; ks < WTH; ++ks) {   // one tile row (16 pixels) per k-step
+        const int prow = ks * WTW + 8 * half + q4;
+        const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow][pcol]);
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Ps[buf][prow + 4][pcol]);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        const int xcol = wj * 32 + 16 * grp_hi + 4 * p4;
+        // tap fragments are read PF taps ahead of their MFMA (a rolling window of PF+1 fragments:
+        // hoisting all nine would spill), pinned in that order with sched_group_barrier so the LDS
+        // latency hides behind the MFMAs already issued instead of being waited out per MFMA
+        constexpr int PF = 3;
+        auto read_tap = [&](int t) __attribute__((always_inline)) {
+          const int tap = min(tap0 + t, 8);
+          const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+          const int xrow = (ks + dy) * WHW + 8 * half + dx + q4;
+          s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow][xcol]);
+          s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)&Xs[buf][xrow + 4][xcol]);
+          return __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+        };
+        bf16x8 bfr[NTAP];
+  #pragma unroll
+        for (int t = 0; t < PF && t < NTAP; ++t) bfr[t] = read_tap(t);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * PF, 0);
+  #pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+          if (t < NTP) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[t], acc[t], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (t + PF < NTAP) {
+            bfr[t + PF] = read_tap(t + PF);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
         }
       }
+      if (more) store_tile(pt + 1, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
     }
-    if (more) store_tile(pt + 1, buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
-  }
+  };
+  if (TG == 1) tile_loop(std::integral_constant<int, 9>{});
+  else if (tg == 0) tile_loop(std::integral_constant<int, 5>{});
+  else tile_loop(std::integral_constant<int, 4>{});
 
   const int ctot = Q.Ctot;
 #pragma unroll
@@ -1505,78 +1513,82 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
   for (int t = 0; t < 6; ++t) acc[t] = f32x16{};
 
   // raw operands of one k-step: δ0, δ1 of the lane's pair and the seven d_j rows its planes use
-  // (group 0: dy 0 d0..d3, dy 1 d0..d2; group 1: dy 1 d1..d3, dy 2 d0..d3)
+  // (group 0: dy 0 d0..d3, dy 1 d0..d2; group 1: dy 1 d1..d3, dy 2 d0..d3). The plane group is a
+  // template constant of the whole tile loop (tile_loop below): a per-k-step branch on it splits the
+  // loop into blocks at whose joins the compiler drains the LDS counter, serialising the next
+  // k-step's reads behind the current MFMAs.
   struct Frag {
     float a0, a1, d[7];
   };
-  const int dy_a = tg == 0 ? 0 : 1;   // row of the first four d (group 0: dy 0; group 1: dy 1 from j = 1)
-  auto frag = [&](int buf, int ks) __attribute__((always_inline)) {
-    Frag f;
-    const int pp = 2 * ks + half, r = pp / PPR, c2 = pp % PPR;
-    const float* pr = &Ps[buf][r * WTW + 2 * c2][wc * 32 + l32];
-    f.a0 = pr[0];
-    f.a1 = pr[BI];
-    const float* xr = &Xs[buf][r * WHW + 2 * c2][wj * 32 + l32];
-    if (tg == 0) {
+  auto tile_loop = [&](auto tgc) __attribute__((always_inline)) {
+    constexpr int TG = decltype(tgc)::value;
+    auto frag = [&](int buf, int ks) __attribute__((always_inline)) {
+      Frag f;
+      const int pp = 2 * ks + half, r = pp / PPR, c2 = pp % PPR;
+      const float* pr = &Ps[buf][r * WTW + 2 * c2][wc * 32 + l32];
+      f.a0 = pr[0];
+      f.a1 = pr[BI];
+      const float* xr = &Xs[buf][r * WHW + 2 * c2][wj * 32 + l32];
+      if constexpr (TG == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) f.d[j] = xr[j * CJ];            // dy 0
+        for (int j = 0; j < 4; ++j) f.d[j] = xr[j * CJ];              // dy 0
 #pragma unroll
-      for (int j = 0; j < 3; ++j) f.d[4 + j] = xr[(WHW + j) * CJ];  // dy 1, j = 0..2
-    } else {
+        for (int j = 0; j < 3; ++j) f.d[4 + j] = xr[(WHW + j) * CJ];  // dy 1, j = 0..2
+      } else {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) f.d[j] = xr[(WHW + 1 + j) * CJ];  // dy 1, j = 1..3
+        for (int j = 0; j < 3; ++j) f.d[j] = xr[(WHW + 1 + j) * CJ];      // dy 1, j = 1..3
 #pragma unroll
-      for (int j = 0; j < 4; ++j) f.d[3 + j] = xr[(2 * WHW + j) * CJ];  // dy 2
+        for (int j = 0; j < 4; ++j) f.d[3 + j] = xr[(2 * WHW + j) * CJ];  // dy 2
+      }
+      return f;
+    };
+    auto mma = [&](const Frag& f) __attribute__((always_inline)) {
+      const float A0 = f.a0, A1 = f.a0 + f.a1, A2 = f.a0 - f.a1, A3 = -f.a1;
+      const float* d = f.d;
+      if constexpr (TG == 0) {  // dy 0: d[0..3]; dy 1: d[4..6] = d0..d2
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[0] - d[2], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[1] + d[2], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[2] - d[1], acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[1] - d[3], acc[3], 0, 0, 0);
+        acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[4] - d[6], acc[4], 0, 0, 0);
+        acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[5] + d[6], acc[5], 0, 0, 0);
+      } else {  // dy 1: d[0..2] = d1..d3; dy 2: d[3..6] = d0..d3
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[1] - d[0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[0] - d[2], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[3] - d[5], acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[4] + d[5], acc[3], 0, 0, 0);
+        acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[5] - d[4], acc[4], 0, 0, 0);
+        acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[4] - d[6], acc[5], 0, 0, 0);
+      }
+    };
+    if (pt_begin < pt_end) {
+      load_p((int)pt_begin);
+      load_x((int)pt_begin);
     }
-    return f;
-  };
-  (void)dy_a;
-  auto mma = [&](const Frag& f) __attribute__((always_inline)) {
-    const float A0 = f.a0, A1 = f.a0 + f.a1, A2 = f.a0 - f.a1, A3 = -f.a1;
-    if (tg == 0) {
-      const float* d = f.d;  // dy 0: d[0..3]; dy 1: d[4..6] = d0..d2
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[0] - d[2], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[1] + d[2], acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[2] - d[1], acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[1] - d[3], acc[3], 0, 0, 0);
-      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[4] - d[6], acc[4], 0, 0, 0);
-      acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[5] + d[6], acc[5], 0, 0, 0);
-    } else {
-      const float* d = f.d;  // dy 1: d[0..2] = d1..d3; dy 2: d[3..6] = d0..d3
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[1] - d[0], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[0] - d[2], acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[3] - d[5], acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[4] + d[5], acc[3], 0, 0, 0);
-      acc[4] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[5] - d[4], acc[4], 0, 0, 0);
-      acc[5] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[4] - d[6], acc[5], 0, 0, 0);
+    __syncthreads();  // coefficients visible
+    if (pt_begin < pt_end) {
+      store_p((int)pt_begin, 0);
+      store_x((int)pt_begin, 0);
     }
-  };
-
-  if (pt_begin < pt_end) {
-    load_p((int)pt_begin);
-    load_x((int)pt_begin);
-  }
-  __syncthreads();  // coefficients visible
-  if (pt_begin < pt_end) {
-    store_p((int)pt_begin, 0);
-    store_x((int)pt_begin, 0);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
-    const bool more = pt + 1 < (int)pt_end;
-    if (more) { load_p(pt + 1); load_x(pt + 1); }
-    Frag cur = frag(buf, 0);
-#pragma unroll 4
-    for (int ks = 0; ks < KS; ++ks) {
-      const Frag nxt = frag(buf, ks + 1 < KS ? ks + 1 : 0);
-      mma(cur);
-      cur = nxt;
-    }
-    if (more) { store_p(pt + 1, buf ^ 1); store_x(pt + 1, buf ^ 1); }
     __syncthreads();
-    buf ^= 1;
-  }
+    int buf = 0;
+    for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+      const bool more = pt + 1 < (int)pt_end;
+      if (more) { load_p(pt + 1); load_x(pt + 1); }
+      Frag cur = frag(buf, 0);
+#pragma unroll 4
+      for (int ks = 0; ks < KS; ++ks) {
+        const Frag nxt = frag(buf, ks + 1 < KS ? ks + 1 : 0);
+        mma(cur);
+        cur = nxt;
+      }
+      if (more) { store_p(pt + 1, buf ^ 1); store_x(pt + 1, buf ^ 1); }
+      __syncthreads();
+      buf ^= 1;
+    }
+  };
+  if (tg == 0) tile_loop(std::integral_constant<int, 0>{});
+  else tile_loop(std::integral_constant<int, 1>{});
 
   // planes of this wave: group 0 -> 0..5, group 1 -> 6..11 (plane = dy * 4 + xi)
   int ln = lane;
