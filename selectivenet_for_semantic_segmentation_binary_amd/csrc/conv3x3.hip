@@ -1381,20 +1381,24 @@ conv3x3_wgrad_halo_f32_kernel(GatherArg P, GatherArg Q, float* __restrict__ out,
 // fixed-order split reduction applies the output transform (wgrad_wino_reduce_kernel, gemm.hip).
 // Tiles are staged as in conv3x3_wgrad_halo_f32_kernel (double-buffered, next tile loaded during
 // the MFMAs, BN+ReLU of the producer applied at the LDS write).
-template <int TWW>
-__global__ void __launch_bounds__(512, 1)
+// NW = 8 waves (2 plane groups of 6: dy 0 + dy 1 xi 0-1 / dy 1 xi 2-3 + dy 2) or 12 waves (3 plane
+// groups, one kernel row dy each: 4 accumulators, 6 LDS reads per 4 MFMAs, three waves per SIMD)
+template <int TWW, int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
 conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chunks, int64_t tiles_per_split,
                               int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
                               int ldw) {
   constexpr int BI = 64, CJ = 64;
   // pixel tile 8 x TWW (TWW = 16: 64 output pairs, 32 k-steps per tile, half the per-tile overhead of 8 x 8)
   constexpr int WTH = FTH, WTW = TWW, WHW = TWW + 2, WPIXT = FTH * TWW, WHP = (FTH + 2) * (TWW + 2);
-  constexpr int NT = 512;
-  constexpr int P_ROUNDS = (WPIXT * BI / 4) / NT;
+  constexpr int NT = NW * 64;
+  constexpr int P_VEC = WPIXT * BI / 4;
+  constexpr int P_ROUNDS = (P_VEC + NT - 1) / NT;
   constexpr int X_ROUNDS = (WHP * (CJ / 4) + NT - 1) / NT;
+  constexpr int NACC = NW == 8 ? 6 : 4;  // planes per wave
   constexpr int KS = WPIXT / 4;  // k-steps per tile: two pairs per k-step
   constexpr int PPR = TWW / 2;   // pairs per tile row
-  static_assert(P_ROUNDS * NT == WPIXT * BI / 4, "dY tile must split evenly over the threads");
+  static_assert(NW == 8 || NW == 12, "8 or 12 waves");
 
   __shared__ __attribute__((aligned(16))) float Ps[2][WPIXT][BI];
   __shared__ __attribute__((aligned(16))) float Xs[2][WHP][CJ];
@@ -1404,7 +1408,7 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
   const int lane = tid & 63, wave = tid >> 6;
   const int wj = wave & 1;          // ci half
   const int wc = (wave >> 1) & 1;   // co half
-  const int tg = wave >> 2;         // plane group
+  const int tg = wave >> 2;         // plane group (NW = 12: the kernel row dy)
   const int half = lane >> 5, l32 = lane & 31;
 
   const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -1459,7 +1463,7 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
     tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
-      const int idx = r * NT + tid;
+      const int idx = min(r * NT + tid, P_VEC - 1);
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const int y = min(y0 + px / WTW, H - 1), x = min(x0 + px % WTW, W - 1);
       rp[r] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(pa.data) +
@@ -1484,6 +1488,7 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
       const int idx = r * NT + tid;
+      if (P_VEC % NT != 0 && idx >= P_VEC) continue;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
       if (y0 + px / WTW < H && x0 + px % WTW < W)
@@ -1508,9 +1513,9 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
     }
   };
 
-  f32x16 acc[6];
+  f32x16 acc[NACC];
 #pragma unroll
-  for (int t = 0; t < 6; ++t) acc[t] = f32x16{};
+  for (int t = 0; t < NACC; ++t) acc[t] = f32x16{};
 
   // raw operands of one k-step: δ0, δ1 of the lane's pair and the seven d_j rows its planes use
   // (group 0: dy 0 d0..d3, dy 1 d0..d2; group 1: dy 1 d1..d3, dy 2 d0..d3). The plane group is a
@@ -1529,7 +1534,10 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
       f.a0 = pr[0];
       f.a1 = pr[BI];
       const float* xr = &Xs[buf][r * WHW + 2 * c2][wj * 32 + l32];
-      if constexpr (TG == 0) {
+      if constexpr (NW == 12) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f.d[j] = xr[(TG * WHW + j) * CJ];  // dy = TG: d0..d3
+      } else if constexpr (TG == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) f.d[j] = xr[j * CJ];              // dy 0
 #pragma unroll
@@ -1545,7 +1553,12 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
     auto mma = [&](const Frag& f) __attribute__((always_inline)) {
       const float A0 = f.a0, A1 = f.a0 + f.a1, A2 = f.a0 - f.a1, A3 = -f.a1;
       const float* d = f.d;
-      if constexpr (TG == 0) {  // dy 0: d[0..3]; dy 1: d[4..6] = d0..d2
+      if constexpr (NW == 12) {  // one kernel row: xi 0..3
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[0] - d[2], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[1] + d[2], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[2] - d[1], acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(A3, d[1] - d[3], acc[3], 0, 0, 0);
+      } else if constexpr (TG == 0) {  // dy 0: d[0..3]; dy 1: d[4..6] = d0..d2
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0, d[0] - d[2], acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1, d[1] + d[2], acc[1], 0, 0, 0);
         acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(A2, d[2] - d[1], acc[2], 0, 0, 0);
@@ -1588,15 +1601,16 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
     }
   };
   if (tg == 0) tile_loop(std::integral_constant<int, 0>{});
-  else tile_loop(std::integral_constant<int, 1>{});
+  else if (NW == 8 || tg == 1) tile_loop(std::integral_constant<int, 1>{});
+  else tile_loop(std::integral_constant<int, 2>{});
 
   // planes of this wave: group 0 -> 0..5, group 1 -> 6..11 (plane = dy * 4 + xi)
   int ln = lane;
   asm volatile("" : "+v"(ln));
   const int ctot = Q.Ctot;
 #pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const int plane = tg * 6 + t;
+  for (int t = 0; t < NACC; ++t) {
+    const int plane = tg * NACC + t;
     const int j = plane * ctot + c0 + wj * 32 + (ln & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1644,9 +1658,14 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
   int64_t per;
   const int64_t splits = conv3x3_wgrad_wino_splits(p, q, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
-  auto kern = tw == 8 ? conv3x3_wgrad_wino_f32_kernel<8> : conv3x3_wgrad_wino_f32_kernel<16>;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(512), 0, st, p, q, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
-                     ws, (int64_t)p.K * ldw, ldw);
+  static const int nw = [] {
+    const char* v = getenv("SELUNET_WINO_WGRAD_WAVES");
+    return v && atoi(v) == 8 ? 8 : 12;
+  }();
+  auto kern = tw == 8 ? (nw == 8 ? conv3x3_wgrad_wino_f32_kernel<8, 8> : conv3x3_wgrad_wino_f32_kernel<8, 12>)
+                      : (nw == 8 ? conv3x3_wgrad_wino_f32_kernel<16, 8> : conv3x3_wgrad_wino_f32_kernel<16, 12>);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(nw * 64), 0, st, p, q, co_tiles, ci_chunks, per, tiles_x, tiles_y,
+                     total, ws, (int64_t)p.K * ldw, ldw);
   return check_launch("conv3x3_wgrad_wino");
 }
 
