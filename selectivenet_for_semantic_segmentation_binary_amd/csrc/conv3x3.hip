@@ -1592,6 +1592,9 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
 #pragma unroll 4
       for (int ks = 0; ks < KS; ++ks) {
         const Frag nxt = frag(buf, ks + 1 < KS ? ks + 1 : 0);
+        // the next k-step's LDS reads stay ahead of this one's MFMAs (left alone, the scheduler sinks
+        // them next to their use across the unrolled k-steps and waits each out with lgkmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
         mma(cur);
         cur = nxt;
       }
