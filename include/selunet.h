@@ -101,6 +101,9 @@ typedef struct selunet_epilogue {
   float* colsum;
   /* PLAIN only: BatchNorm-backward sums of the written tile, slab [stats_rows][3][N]. */
   selunet_bn_bwd_stats bnb;
+  /* nullable: max |stored value| folded into *amax with an atomic max (float bits; the caller zeroes
+   * it): the range word of a split-fp16 operand (selunet_conv3x3_x2) read by the next layer. */
+  float* amax;
 } selunet_epilogue;
 
 const char* selunet_last_error(void);
@@ -137,6 +140,27 @@ int32_t selunet_conv3x3_wino_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_sr
 int selunet_conv3x3_wino(const selunet_gather* a, const float* u, int32_t n_cols,
                          const selunet_epilogue* ep, void* stream);
 const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
+/* fp32 3x3 conv forward / data gradient (model.py:11 and its input gradient) on the fp16 matrix
+ * cores: each fp32 operand is split into two fp16 parts, v*2^e = h + l (22 significant bits,
+ * 2^e a power of two that keeps the operand below 2^14), and every product is summed as
+ * h_a*h_b + h_a*l_b + l_a*h_b in fp32 accumulators (three v_mfma_f32_32x32x16_f16 per 16-channel
+ * step; the dropped l_a*l_b is below 2^-22 of the product). Measured relative RMS error against
+ * fp64 at K = 576..4608 is at or below the exact fp32 MFMA's (tools/split_probe.hip). Operand
+ * ranges: amax0 / amax1 (device words, amax1 only for a two-source gather) bound |source value
+ * after its BN+ReLU transform|: selunet_act_bound for a BN+ReLU source, the producing kernel's
+ * atomic max (selunet_epilogue.amax, selunet_bn_bwd_apply) otherwise. w: a
+ * SELUNET_PACK_CONV3X3_X2 pack ([n_cols][9*C] + n_cols row unscale factors). Same gathers,
+ * epilogues and statistics slab rows as selunet_gemm_gather; selunet_conv3x3_x2_ok tells whether a
+ * layer can take it (h, w >= 16, C and c_src0 multiples of 32, C > 32, n_cols a multiple of 64). */
+int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
+int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
+                       const float* amax0, const float* amax1, void* stream);
+const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
+/* Range word of a training-mode BatchNorm+ReLU output relu(gamma*xhat + beta) over `count` values
+ * per channel: |xhat| <= sqrt(count - 1) for batch statistics (Samuelson's inequality), so
+ * *out = max_c |gamma_c| * sqrt(count) + max_c |beta_c| bounds every element (max-pooled copies
+ * included). One block; c <= 4096. */
+int selunet_act_bound(const float* gamma, const float* beta, int32_t c, int64_t count, float* out, void* stream);
 /* Rows of the stats slab selunet_gemm_gather writes for this operand (workgroup rows of the
  * kernel it dispatches to: 16x16 halo tiles for single-chunk 3x3 operands, the persistent
  * workgroups of the multi-chunk halo kernel, else 128-row tiles); -1 on error. */
@@ -187,7 +211,12 @@ int32_t selunet_wgrad_ld(int32_t kq);
 #define SELUNET_PACK_MAX 24
 /* SELUNET_PACK_CONV3X3_WINO (fp32): fwd = [co][12*ci] and dgrad = [ci][12*co] Winograd weight
  * operands of selunet_conv3x3_wino (k_pad = 12*ci; dgrad from the flipped/transposed kernel). */
-enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1, SELUNET_PACK_CONV3X3_WINO = 2 };
+/* SELUNET_PACK_CONV3X3_X2 (fp32): split-fp16 operands of selunet_conv3x3_x2, k_pad = 9*ci; fwd =
+ * [co][9*ci] and dgrad = [ci][9*co] 32-bit words (taps flipped), each row scaled by 2^e_row
+ * (max|w_row| * 2^e_row < 2^14) and every 32-k group (one tap, 32 channels) stored as 32 fp16 high
+ * parts h = fp16(v) then 32 low parts l = fp16(v - h); the row unscale factors 2^-e_row follow the
+ * matrix: fwd + co*9*ci (co floats), dgrad + ci*9*co (ci floats). ci, co multiples of 32. */
+enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1, SELUNET_PACK_CONV3X3_WINO = 2, SELUNET_PACK_CONV3X3_X2 = 3 };
 typedef struct selunet_pack_desc {
   const float* w;
   void* fwd;
@@ -264,6 +293,11 @@ int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, d
 int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
                          const float* shift, const float* mean, const float* invstd,
                          const float* coef, void* dy, int32_t dtype, void* stream);
+/* The same with max|dy| folded into *amax (atomic max on the float bits; zeroed by the caller):
+ * the range word of dy as a split-fp16 operand (selunet_conv3x3_x2, split-fp16 weight gradient). */
+int selunet_bn_bwd_apply_amax(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
+                              const float* shift, const float* mean, const float* invstd,
+                              const float* coef, void* dy, float* amax, int32_t dtype, void* stream);
 
 /* Stream-ordered device memset / device-to-device copy (hipMemsetAsync / hipMemcpyAsync):
  * zeroing atomic-accumulation targets and gathering small parameter vectors inside a recorded

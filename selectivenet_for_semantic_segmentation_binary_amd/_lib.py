@@ -40,7 +40,8 @@ class BnBwdStats(ctypes.Structure):
 
 class Epilogue(ctypes.Structure):
     _fields_ = [("out0", c_void_p), ("out1", c_void_p), ("bias", c_void_p), ("stats", c_void_p),
-                ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats)]
+                ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats),
+                ("amax", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -48,7 +49,7 @@ class PackDesc(ctypes.Structure):
                 ("ci", c_int32), ("k_pad", c_int32), ("offset", c_int64)]
 
 
-PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO = 24, 0, 1, 2
+PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2 = 24, 0, 1, 2, 3
 WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
 
 
@@ -86,6 +87,10 @@ SIGNATURES = {
     "selunet_conv3x3_wino_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "selunet_conv3x3_wino": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P]),
     "selunet_conv3x3_wino_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
+    "selunet_conv3x3_x2_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "selunet_conv3x3_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
+    "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
+    "selunet_act_bound": (c_int32, [P, P, c_int32, c_int64, P, P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
     "selunet_set_gather_workgroups": (c_int32, [c_int32]),
@@ -107,6 +112,7 @@ SIGNATURES = {
                                                      c_float, c_float, P, P, P, P, P]),
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
+    "selunet_bn_bwd_apply_amax": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, P, c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),
     "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
     "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P,

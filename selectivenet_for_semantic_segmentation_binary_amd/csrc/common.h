@@ -16,6 +16,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ error state (host)
 void set_error(const char* fmt, ...);
@@ -66,6 +68,32 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// *amax = max(*amax, wave max of v >= 0) as one atomic per wave on the float bits (non-negative
+// floats order like their bit patterns; a NaN propagates as the largest). Every lane calls it.
+__device__ __forceinline__ void atomic_amax(float* amax, float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(v));
+}
+
+// Power-of-two scale 2^e of a split-fp16 operand whose magnitudes are bounded by amax:
+// amax * 2^e < 2^14, so the high part fp16(v * 2^e) and the low part fp16(v * 2^e - high) stay far
+// below the fp16 maximum (65504) while small values keep their bits above the fp16 subnormal floor.
+// amax = 0 (an all-zero operand) gives 2^14. unscale (nullable) receives 2^-e.
+__device__ __forceinline__ float x2_scale(float amax, float* unscale) {
+  int e = 0;
+  if (amax > 0.0f) frexpf(amax, &e);  // amax < 2^e
+  e = min(max(14 - e, -100), 100);
+  if (unscale) *unscale = ldexpf(1.0f, -e);
+  return ldexpf(1.0f, e);
+}
+
+// v -> (high, low) fp16 parts of v (already scaled): v = high + low to 22 significant bits
+__device__ __forceinline__ void x2_split(float v, _Float16& h, _Float16& l) {
+  h = (_Float16)v;
+  l = (_Float16)(v - (float)h);
 }
 
 }  // namespace selunet

@@ -289,10 +289,22 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
 // until the epilogue of tile i (which uses the whole LDS) is done, then go to LDS. The epilogue's
 // column sums (BN statistics / colsum / BN-backward sums) accumulate in registers over the tiles
 // and are reduced once: one slab row per workgroup (row prow, see conv3x3_halo_stats_rows).
-template <typename T, int BN>
+//
+// X2 (fp32 sources only): the split-fp16 form of the fp32 convolution (selunet_conv3x3_x2). The halo
+// stager scales every transformed value by 2^e (from the operand range words amax0/amax1) and
+// writes it as two fp16 parts into the same 128-B pixel row a 32-channel fp32 chunk occupies:
+// bytes 0-63 the 32 high parts, 64-127 the 32 low parts, so 16-B units q = 0, 1 hold the high
+// parts of the two 16-channel k-steps and q = 2, 3 their low parts. The weights
+// (SELUNET_PACK_CONV3X3_X2) have the same 128-B layout per (tap, chunk) and are staged unchanged.
+// Per tap: 2 k-steps x 3 v_mfma_f32_32x32x16_f16 (hh, hl, lh) per 32x32 subtile instead of 16 fp32
+// MFMAs (32 vs 64 cycles each: 5.3x fewer MFMA cycles); the accumulators are unscaled by
+// 2^-e * (row unscale of the weights) before the epilogue.
+template <typename T, int BN, bool X2>
 __global__ void __launch_bounds__(HTHREADS, 1)
 conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles,
-                            int tiles_x, int tiles_y, int ptiles, int gp) {
+                            int tiles_x, int tiles_y, int ptiles, int gp, const float* __restrict__ wcs,
+                            const float* __restrict__ amax0, const float* __restrict__ amax1) {
+  static_assert(!X2 || std::is_same<T, float>::value, "split-fp16 form of fp32 operands only");
   constexpr int E = 16 / sizeof(T);
   constexpr int CK = 128 / sizeof(T);
   constexpr int WAVES_N = BN / 64;
@@ -327,6 +339,37 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   const int ntl = prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0;  // host: gp <= ptiles, so >= 1
   const int nchunks = g.Ctot / CK;
   const int csteps = nchunks * 9;  // steps per tile
+  float xs = 1.0f;       // X2: operand scale 2^e
+  float cfac[NT] = {};   // X2: accumulator unscale per 32-column subtile (this lane's column)
+  if constexpr (X2) {
+    float am = amax0 ? amax0[0] : 0.0f;
+    if (g.nsrc > 1 && amax1) am = fmaxf(am, amax1[0]);
+    float inv;
+    xs = x2_scale(am, &inv);
+#pragma unroll
+    for (int b = 0; b < NT; ++b) cfac[b] = wcs[n0 + wn * 64 + b * 32 + l32] * inv;
+  }
+  // one 16-B halo slice (4 transformed fp32 values or E raw elements) to halo buffer hb
+  auto halo_store = [&](int hb, int hp, int cc, uint4 v) __attribute__((always_inline)) {
+    unsigned char* base = As + hb * HPIX * AROWB + hp * AROWB;
+    if constexpr (X2) {
+      float f[4];
+      __builtin_memcpy(f, &v, 16);
+      f16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        _Float16 a, b;
+        x2_split(f[e] * xs, a, b);
+        h[e] = a;
+        l[e] = b;
+      }
+      const int par = (hp / HWT) & 1;
+      *reinterpret_cast<f16x4*>(base + (((cc >> 1) ^ par) << 4) + (cc & 1) * 8) = h;
+      *reinterpret_cast<f16x4*>(base + (((4 + (cc >> 1)) ^ par) << 4) + (cc & 1) * 8) = l;
+    } else {
+      *reinterpret_cast<uint4*>(base + (((cc ^ ((hp / HWT) & 1))) << 4)) = v;
+    }
+  };
 
   auto tile_xy = [&](int i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
     const unsigned pt = (unsigned)(prow + i * gp);
@@ -400,6 +443,33 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     const unsigned char* b_src = Bs + bbuf * BN * ROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
+    if constexpr (X2) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        f16x8 ah[MT], al[MT], bh[NT], bl[NT];
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          const unsigned char* p = a_src + (hrow0[a] + tap_off) * AROWB + ((hsw0[a] ^ dy) & 1) * 16;
+          ah[a] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          al[a] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const unsigned char* p = b_src + (wn * 64 + b * 32 + l32) * ROWB + half * 16;
+          bh[b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          bl[b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      }
+      return;
+    }
 #if (SELUNET_ABL & 1)
     uint4 af[4][MT], bfr[4][NT];
 #pragma unroll
@@ -451,7 +521,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     if (!a_slot(r, hp, cc)) return;
     uint4 o = make_uint4(0, 0, 0, 0);
     if (a_inside(y0, x0, hp)) o = sa.scale ? transform16<T>(v, sa.scale, sa.shift, c + cc * E, sa.relu) : v;
-    *reinterpret_cast<uint4*>(As + hb * HPIX * AROWB + halo_off(hp, cc)) = o;
+    halo_store(hb, hp, cc, o);
   };
 
   // ---------------------------------------------------------------- prologue: tile 0 chunk 0, B(0), B(1)
@@ -475,7 +545,8 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   rb_next = b_load(1 % csteps);
   __syncthreads();
 
-  using Acc = typename StatAcc<T>::type;
+  // (X2 at BN = 128: fp32 statistics registers, as the Winograd kernel — fp64 ones spill)
+  using Acc = std::conditional_t<X2 && BN == 128, float, typename StatAcc<T>::type>;
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const TileStats ts = tile_stats(ep, prow, n0, N);
@@ -541,7 +612,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
                   __builtin_memcpy(&v, e, 16);
                 }
               }
-              *reinterpret_cast<uint4*>(As + ((J + 1) & 1) * HPIX * AROWB + halo_off(hp, cc)) = v;
+              halo_store((J + 1) & 1, hp, cc, v);
             }
           }
         }
@@ -555,6 +626,12 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     }
 
     // ------------------------------------------------------------ epilogue of tile i
+    if constexpr (X2) {
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] *= cfac[b];
+    }
     acc_to_lds<MT, NT, BN>(tile, acc, wm * WPIX, wn * 64, lane);
 #pragma unroll
     for (int a = 0; a < MT; ++a)
@@ -1791,9 +1868,9 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   if (!one && persist_enabled()) {
     const int dtype = sizeof(T) == 2 ? SELUNET_BF16 : SELUNET_F32;
     const int gp = (int)conv3x3_halo_stats_rows(g, N, dtype);
-    hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g,
-                       reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
-                       (int)conv3x3_halo_tiles(g), gp);
+    hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN, false>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0,
+                       st, g, reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
+                       (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr);
     return;
   }
   auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
@@ -1836,6 +1913,35 @@ int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg&
   if (conv3x3_wino_bn128(N, ep)) launch_wino<128, 1>(g, u, N, ep, st);
   else launch_wino<64, 2>(g, u, N, ep, st);
   return check_launch("conv3x3_wino");
+}
+
+bool conv3x3_x2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols) {
+  return persist_enabled() && h >= TH && w >= TW && c_in % 32 == 0 && c_src0 % 32 == 0 && c_in > 32 &&
+         n_cols % 64 == 0;
+}
+
+bool conv3x3_x2_eligible(const GatherArg& g, int N) {
+  return conv3x3_halo_eligible(g, N, SELUNET_F32) && conv3x3_halo_persistent(g, SELUNET_F32) &&
+         conv3x3_x2_shape_ok(g.h, g.w, g.Ctot, g.src[0].C, N);
+}
+
+template <int BN>
+static void launch_x2(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                      const float* amax1, hipStream_t st) {
+  const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
+  const int n_tiles = N / BN;
+  const int gp = persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
+  const int k_pad = 9 * g.Ctot;
+  hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0,
+                     st, g, w, N, k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp,
+                     w + (int64_t)N * k_pad, amax0, amax1);
+}
+
+int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                      const float* amax1, hipStream_t st) {
+  if (conv3x3_wino_bn128(N, ep)) launch_x2<128>(g, w, N, ep, amax0, amax1, st);
+  else launch_x2<64>(g, w, N, ep, amax0, amax1, st);
+  return check_launch("conv3x3_x2");
 }
 
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,

@@ -173,6 +173,7 @@ struct EpiArg {
   int split;
   float* colsum;
   BnBwdArg bnb;
+  float* amax;  // nullable: atomic max of |stored value| (float bits), see selunet_epilogue.amax
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -217,6 +218,7 @@ struct TileStats {
   int gcol0;           // global column of tile column 0
   BnBwdArg bnb;        // scale/shift/mean/invstd/slab offset to gcol0; y = base pointer
   const void* out0;    // base of the PLAIN output (to locate y)
+  float* amax;         // nullable: running max |stored value| (atomic, float bits)
 };
 
 // The statistics outputs of workgroup (slab row `row`, first global column n0) of an N-column GEMM.
@@ -236,6 +238,7 @@ __device__ __forceinline__ TileStats tile_stats(const EpiArg& ep, int64_t row, i
     ts.bnb.slab += row * 3 * N + n0;
   }
   ts.out0 = ep.out0;
+  ts.amax = ep.amax;
   return ts;
 }
 
@@ -288,6 +291,7 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
   float* t1 = WIDE ? tw1 : reinterpret_cast<float*>(s1);
   float* t2 = WIDE ? tw2 : reinterpret_cast<float*>(s2);
   float* t3 = WIDE ? tw3 : reinterpret_cast<float*>(s3);
+  float am = 0.0f;
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
@@ -306,6 +310,10 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
     T o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = from_f<T>(v[e]);
+    if (ts.amax) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(to_f(o[e])));
+    }
     if constexpr (sizeof(T) == 2) {
       uint4 u;
       __builtin_memcpy(&u, o, 16);
@@ -340,6 +348,7 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       }
     }
   }
+  if (ts.amax) atomic_amax(ts.amax, am);
   if constexpr (WIDE) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -415,6 +424,11 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
 bool conv3x3_wino_eligible(const GatherArg& g, int N);
 bool conv3x3_wino_bn128(int N, const EpiArg& ep);
 int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st);
+// fp32 forward / data gradient on split-fp16 operands (conv3x3.hip, selunet_conv3x3_x2)
+bool conv3x3_x2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
+bool conv3x3_x2_eligible(const GatherArg& g, int N);
+int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                      const float* amax1, hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
                               hipStream_t st);

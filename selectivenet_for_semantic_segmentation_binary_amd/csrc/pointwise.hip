@@ -153,6 +153,53 @@ __global__ void pack_weights_kernel(selunet_pack_list l, int64_t total) {
   }
 }
 
+// Split-fp16 ("x2") operands of the fp32 3x3 convolutions (SELUNET_PACK_CONV3X3_X2): one block per
+// matrix row (fwd: output channel o, k = tap*ci + c; dgrad: input channel c, k = tap*co + o, taps
+// flipped). The row is scaled by 2^e (max|w_row| * 2^e < 2^14, so both fp16 parts stay normal-range)
+// and every 32-k group is stored as 32 fp16 high parts h = fp16(v) then 32 low parts
+// l = fp16(v - h): v = h + l to 22 significant bits. The row's unscale factor 2^-e follows the
+// matrix (fwd + co*9*ci, dgrad + ci*9*co). desc.offset = first block (row) of the entry.
+__global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
+  int t = 0;
+  const int64_t b = blockIdx.x;
+  while (t + 1 < l.n && b >= l.d[t + 1].offset) ++t;
+  const selunet_pack_desc& d = l.d[t];
+  const int co = d.co, ci = d.ci;
+  const int r = (int)(b - d.offset);
+  const bool fw = r < co;
+  const int row = fw ? r : r - co;
+  const int len = fw ? 9 * ci : 9 * co;
+  const int rk = fw ? ci : co;  // k = tap * rk + channel
+  const float* w = d.w;
+  auto val = [&](int k) -> float {
+    const int tap = k / rk, c = k - tap * rk;
+    return fw ? w[((int64_t)row * ci + c) * 9 + tap] : w[((int64_t)c * ci + row) * 9 + (8 - tap)];
+  };
+  float m = 0.0f;
+  for (int k = threadIdx.x; k < len; k += 256) m = fmaxf(m, fabsf(val(k)));
+  __shared__ float red[256];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  float* base = reinterpret_cast<float*>(fw ? d.fwd : d.dgrad);
+  const int rows = fw ? co : ci;
+  float unscale;
+  const float sc = x2_scale(red[0], &unscale);
+  _Float16* out = reinterpret_cast<_Float16*>(base + (int64_t)row * len);
+  for (int k = threadIdx.x; k < len; k += 256) {
+    const float v = val(k) * sc;
+    const _Float16 h = (_Float16)v;
+    const _Float16 lo = (_Float16)(v - (float)h);
+    const int grp = k >> 5, j = k & 31;
+    out[grp * 64 + j] = h;
+    out[grp * 64 + 32 + j] = lo;
+  }
+  if (threadIdx.x == 0) base[(int64_t)rows * len + row] = unscale;
+}
+
 static unsigned grid_for(int64_t n, int64_t cap = 4096) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, TPB), cap));
 }
@@ -452,7 +499,7 @@ template <typename T, int U = 4>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                     const float* __restrict__ mean, const float* __restrict__ invstd,
-                                    const float* __restrict__ coef, T* __restrict__ dy) {
+                                    const float* __restrict__ coef, T* __restrict__ dy, float* amax) {
   const int CG = C >> 3;
   const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
   const int PL = TPB / CG;
@@ -469,12 +516,17 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
   }
   // U pixels per thread and iteration, all loads issued before any use (loads in flight per wave)
   const int64_t stride = (int64_t)gridDim.x * PL;
+  float am = 0.0f;
   auto one = [&](const f32x4& y0, const f32x4& y1, const f32x4& g0, const f32x4& g1, int64_t off) {
     f32x4 o0, o1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       o0[e] = (y0[e] * sc[e] + sh[e] > 0.0f ? k0[e] * g0[e] : 0.0f) - b[e] - a[e] * y0[e];
       o1[e] = (y1[e] * sc[e + 4] + sh[e + 4] > 0.0f ? k0[e + 4] * g1[e] : 0.0f) - b[e + 4] - a[e + 4] * y1[e];
+    }
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = fmaxf(am, fmaxf(fabsf(o0[e]), fabsf(o1[e])));
     }
     Vec4<T>::store(dy + off, o0);
     Vec4<T>::store(dy + off + 4, o1);
@@ -498,6 +550,30 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
     one(Vec4<T>::load(y + off), Vec4<T>::load(y + off + 4), Vec4<T>::load(dz + off), Vec4<T>::load(dz + off + 4),
         off);
   }
+  if (amax) atomic_amax(amax, am);
+}
+
+// selunet_act_bound: max_c |gamma_c| * sqrt(count) + max_c |beta_c| (one block)
+__global__ void __launch_bounds__(256) act_bound_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        int C, float sq, float* out) {
+  float g = 0.0f, b = 0.0f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    g = fmaxf(g, fabsf(gamma[c]));
+    b = fmaxf(b, fabsf(beta[c]));
+  }
+  __shared__ float red[2][256];
+  red[0][threadIdx.x] = g;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + s]);
+      red[1][threadIdx.x] = fmaxf(red[1][threadIdx.x], red[1][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  // rounded up a little: the bound must hold for the fp32 values the loaders compute
+  if (threadIdx.x == 0) out[0] = (red[0][0] * sq + red[1][0]) * 1.0001f;
 }
 
 // =========================================================================== first-layer im2col
@@ -1171,12 +1247,21 @@ int selunet_pack_convT(const float* w, int32_t ci, int32_t co, void* fwd, void* 
 int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(list && list->n > 0 && list->n <= SELUNET_PACK_MAX, "pack_weights: bad list");
   selunet_pack_list l = *list;
-  int64_t off = 0;
+  selunet_pack_list lx = *list;  // the split-fp16 entries, one block per matrix row
+  lx.n = 0;
+  int64_t off = 0, xrows = 0;
   for (int t = 0; t < l.n; ++t) {
     selunet_pack_desc& d = l.d[t];
     SELUNET_REQUIRE(d.w && (d.fwd || d.dgrad) && d.co > 0 && d.ci > 0, "pack_weights: bad entry %d", t);
     d.offset = off;
-    if (d.kind == SELUNET_PACK_CONV3X3) {
+    if (d.kind == SELUNET_PACK_CONV3X3_X2) {
+      SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == 9 * d.ci && d.ci % 32 == 0 && d.co % 32 == 0,
+                      "pack_weights: split-fp16 entry %d needs fp32, fwd, k_pad = 9*ci and ci, co multiples of 32", t);
+      lx.d[lx.n] = d;
+      lx.d[lx.n].offset = xrows;
+      ++lx.n;
+      xrows += d.co + (d.dgrad ? d.ci : 0);
+    } else if (d.kind == SELUNET_PACK_CONV3X3) {
       SELUNET_REQUIRE(d.fwd && d.k_pad >= 9 * d.ci, "pack_weights: bad conv3x3 entry %d", t);
       off += (int64_t)d.co * d.k_pad + (d.dgrad ? (int64_t)d.ci * 9 * d.co : 0);
     } else if (d.kind == SELUNET_PACK_CONV3X3_WINO) {
@@ -1188,8 +1273,10 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
       off += (int64_t)d.ci * d.co * 4;
     }
   }
-  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weights_kernel<T>, dim3(grid_for(off, 8192)), dim3(TPB), 0,
-                                       as_stream(stream), l, off));
+  if (off > 0)
+    DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weights_kernel<T>, dim3(grid_for(off, 8192)), dim3(TPB), 0,
+                                         as_stream(stream), l, off));
+  if (xrows > 0) hipLaunchKernelGGL(pack_x2_kernel, dim3((unsigned)xrows), dim3(256), 0, as_stream(stream), lx);
   return check_launch("pack_weights");
 }
 
@@ -1376,6 +1463,19 @@ int selunet_bn_bwd_finalize(const double* sums, int64_t count, int32_t c, const 
 int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* coef, void* dy, int32_t dtype,
                          void* stream) {
+  return selunet_bn_bwd_apply_amax(dz, y, m, c, scale, shift, mean, invstd, coef, dy, nullptr, dtype, stream);
+}
+
+int selunet_act_bound(const float* gamma, const float* beta, int32_t c, int64_t count, float* out, void* stream) {
+  SELUNET_REQUIRE(gamma && beta && out && c > 0 && c <= 4096 && count > 0, "act_bound: bad arguments");
+  hipLaunchKernelGGL(act_bound_kernel, dim3(1), dim3(256), 0, as_stream(stream), gamma, beta, c,
+                     (float)std::sqrt((double)count), out);
+  return check_launch("act_bound");
+}
+
+int selunet_bn_bwd_apply_amax(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
+                              const float* shift, const float* mean, const float* invstd, const float* coef, void* dy,
+                              float* amax, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
                   "bn_bwd_apply: bad arguments");
   SELUNET_REQUIRE(ok_channels(c), "bn_bwd_apply: C must be 64, 128, 256 or 512 (got %d)", c);
@@ -1384,12 +1484,13 @@ int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, co
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), gcap));
   if (u8) {
     DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(blocks), dim3(TPB), 0, as_stream(stream),
-                                         (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd, coef, (T*)dy));
+                                         (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd, coef, (T*)dy,
+                                         amax));
     return check_launch("bn_bwd_apply");
   }
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(TPB), 0,
                                        as_stream(stream), (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd,
-                                       coef, (T*)dy));
+                                       coef, (T*)dy, amax));
   return check_launch("bn_bwd_apply");
 }
 

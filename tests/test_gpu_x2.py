@@ -1,0 +1,222 @@
+"""fp32 3x3 convolution on split-fp16 operands (selunet_conv3x3_x2, conv3x3_halo_persist_kernel
+<float, BN, X2>) against torch's conv2d / conv2d input gradient in fp64 on the CPU: the weight pack
+(SELUNET_PACK_CONV3X3_X2), forward with the BN-statistics epilogue and torch.cat sources with folded
+BN+ReLU staging, data gradient with the split (ConvTranspose bias column sums) and BN-backward-sums
+epilogues, and the operand range words (selunet_act_bound, selunet_bn_bwd_apply_amax, the
+epilogue's amax).
+
+Tolerance: 2e-6 of the tensor's max magnitude against the fp64 result, as the fp32 Winograd kernel
+(tests/test_gpu_wino.py): v*2^e = h + l holds 22 significant bits per operand and the three fp16
+products are summed in fp32 accumulators 16 at a time, measured at or below the exact fp32 MFMA's
+error (tools/split_probe.hip: relative RMS 3.8e-7 vs 4.3e-7 at K = 1152)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from selectivenet_for_semantic_segmentation_binary_amd import _lib as K
+from tests.test_gpu_kernels import bn_fold, check_bnb_sums, gen, halo_wgs, nchw, nhwc, rel  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 2e-6
+
+
+def pack_x2(w, dgrad=True):
+    """Split-fp16 operands of a conv3x3 weight [co][ci][3][3] through selunet_pack_weights: fwd
+    [co][9*ci] words + co unscale factors, dgrad [ci][9*co] + ci."""
+    co, ci = w.shape[:2]
+    wd = w.to(DEV).contiguous()
+    fwd = torch.empty(co * 9 * ci + co, device=DEV)
+    dg = torch.empty(ci * 9 * co + ci, device=DEV) if dgrad else None
+    pl = K.PackList()
+    pl.d[0] = K.PackDesc(K.ptr(wd), K.ptr(fwd), K.ptr(dg), K.PACK_CONV3X3_X2, co, ci, 9 * ci, 0)
+    pl.n = 1
+    K.call("selunet_pack_weights", pl, K.F32, K.stream_ptr())
+    return fwd, dg
+
+
+def unpack_x2(buf, rows, k):
+    """fp64 [rows][k] matrix a split-fp16 pack holds: (h + l) * unscale."""
+    m = buf[: rows * k].cpu().view(torch.float16).reshape(rows, k // 32, 2, 32).double()
+    v = (m[:, :, 0] + m[:, :, 1]).reshape(rows, k)
+    return v * buf[rows * k:].cpu().double().view(rows, 1)
+
+
+def test_x2_pack():
+    w = gen(64, 96, 3, 3, seed=1, scale=0.1)
+    w[3] *= 1e-3  # rows of very different ranges: one scale per row
+    fwd, dg = pack_x2(w)
+    torch.cuda.synchronize()
+    ref_f = w.double().permute(0, 2, 3, 1).reshape(64, 9 * 96)  # k = tap * ci + c
+    got = unpack_x2(fwd, 64, 9 * 96)
+    floor = lambda r: r.abs().amax(1, keepdim=True) * 2.0 ** -37  # noqa: E731  fp16 subnormal floor
+    assert ((got - ref_f).abs() <= ref_f.abs() * 2.0 ** -21 + floor(ref_f)).all()
+    us = fwd[64 * 9 * 96:].cpu()
+    assert torch.all(torch.log2(us) == torch.round(torch.log2(us)))  # powers of two
+    wt = w.flip(2, 3).transpose(0, 1)  # the data-gradient conv's kernel [ci][co][3][3]
+    ref_d = wt.double().permute(0, 2, 3, 1).reshape(96, 9 * 64)
+    got_d = unpack_x2(dg, 96, 9 * 64)
+    assert ((got_d - ref_d).abs() <= ref_d.abs() * 2.0 ** -21 + floor(ref_d)).all()
+
+
+def test_x2_eligibility():
+    ok = lambda *a: K.query("selunet_conv3x3_x2_ok", *a)  # noqa: E731
+    assert ok(32, 32, 64, 64, 64) == 1
+    assert ok(32, 32, 32, 32, 64) == 0    # one channel chunk
+    assert ok(8, 8, 64, 64, 64) == 0      # below the 16x16 halo tile
+    assert ok(32, 31, 64, 64, 64) == 1    # odd widths are fine (direct form)
+    assert ok(32, 32, 64, 64, 96) == 0
+
+
+def word(v):
+    return torch.tensor([float(v)], device=DEV)
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,n,h,w,xform", [
+    (64, 0, 64, 2, 16, 16, True),
+    (64, 64, 128, 1, 16, 48, True),     # two sources (torch.cat), BN = 128
+    (128, 0, 256, 2, 20, 24, True),     # partial edge tiles
+    (256, 0, 128, 2, 32, 32, False),
+    (128, 128, 64, 1, 32, 16, True),    # two sources, BN = 64
+    (64, 0, 128, 1, 18, 35, True),      # partial tiles in both directions, odd width
+])
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
+    halo_wgs(wgs)
+    x0 = gen(n, cin0, h, w, seed=1)
+    x1 = gen(n, cin1, h, w, seed=2) * 1e-3 if cin1 else None  # sources of different ranges
+    wt = gen(cout, cin0 + cin1, 3, 3, seed=3, scale=0.05)
+    s0, t0 = bn_fold(cin0, 10)
+    a0 = torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)) if xform else x0
+    a = a0
+    if cin1:
+        s1, t1 = bn_fold(cin1, 12)
+        a1 = torch.relu(x1 * s1.view(1, -1, 1, 1) + t1.view(1, -1, 1, 1))
+        a = torch.cat((a0, a1), 1)
+    ref = F.conv2d(a.double(), wt.double(), padding=1)
+    assert K.query("selunet_conv3x3_x2_ok", h, w, cin0 + cin1, cin0, cout) == 1
+    u, _ = pack_x2(wt, dgrad=False)
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    keep = [d(nhwc(x0)), d(s0), d(t0)]  # K.source holds raw pointers: the tensors must stay alive
+    srcs = [K.source(keep[0], cin0, keep[1] if xform else None, keep[2] if xform else None)]
+    am0, am1 = word(a0.abs().max() * 1.5), None
+    if cin1:
+        keep += [d(nhwc(x1)), d(s1), d(t1)]
+        srcs.append(K.source(keep[3], cin1, keep[4], keep[5]))
+        am1 = word(a1.abs().max())
+    M = n * h * w
+    y = torch.empty(M, cout, device=DEV)
+    g = K.gather(n, h, w, 9, *srcs)
+    rows = K.query("selunet_gemm_stats_rows", g, cout, K.F32)
+    stats = torch.empty(rows, 2, cout, device=DEV)
+    ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+    K.call("selunet_conv3x3_x2", g, K.ptr(u), cout, ep, K.ptr(am0), K.ptr(am1), K.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel(nchw(y.cpu(), n, h, w), ref) < TOL
+    st = stats.cpu().double().sum(0)
+    r = ref.permute(1, 0, 2, 3).reshape(cout, -1)
+    assert rel(st[0], r.sum(1)) < TOL and rel(st[1], (r * r).sum(1)) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,split,h,w", [(64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
+                                                (256, 128, 128, 16, 48), (128, 256, 0, 20, 24),
+                                                (512, 256, 256, 16, 16)])
+@pytest.mark.parametrize("wgs", [0, 3])
+def test_x2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+    """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range."""
+    halo_wgs(wgs)
+    n = 2
+    wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
+    dy = gen(n, cout, h, w, seed=7) * 1e-9
+    x = gen(n, cin, h, w, seed=8).double().requires_grad_()
+    (ref,) = torch.autograd.grad(F.conv2d(x, wt.double(), padding=1), x, dy.double())
+    _, dg = pack_x2(wt)
+    M = n * h * w
+    dyd = nhwc(dy).to(DEV)  # kept alive: K.source holds the raw pointer
+    am = word(dy.abs().max())
+    g = K.gather(n, h, w, 9, K.source(dyd, cout))
+    rows = K.query("selunet_gemm_stats_rows", g, cin, K.F32)
+    if split:
+        d0 = torch.empty(M, split, device=DEV)
+        d1 = torch.empty(M, cin - split, device=DEV)
+        colsum = torch.empty(rows, split, device=DEV)
+        ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split, K.ptr(colsum))
+        K.call("selunet_conv3x3_x2", g, K.ptr(dg), cin, ep, K.ptr(am), None, K.stream_ptr())
+        got = torch.cat((nchw(d0.cpu(), n, h, w), nchw(d1.cpu(), n, h, w)), 1)
+        assert rel(colsum.double().sum(0).cpu(), d0.double().sum(0).cpu()) < 1e-6
+    else:
+        dx = torch.empty(M, cin, device=DEV)
+        yprev = gen(M, cin, seed=42).to(DEV)
+        sc, sh = (gen(cin, seed=43).abs() + 0.5).to(DEV), (gen(cin, seed=44) * 0.3).to(DEV)
+        mean, invstd = (gen(cin, seed=45) * 0.1).to(DEV), (gen(cin, seed=46).abs() + 0.5).to(DEV)
+        slab = torch.empty(rows, 3, cin, device=DEV)
+        ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+        ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+        K.call("selunet_conv3x3_x2", g, K.ptr(dg), cin, ep, K.ptr(am), None, K.stream_ptr())
+        got = nchw(dx.cpu(), n, h, w)
+        check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
+    torch.cuda.synchronize()
+    assert rel(got, ref) < TOL
+
+
+def test_x2_rejects():
+    n, h, w, c = 1, 8, 8, 64
+    x = torch.zeros(n * h * w, c, device=DEV)
+    u = torch.zeros(64 * 9 * c + 64, device=DEV)
+    y = torch.empty(n * h * w, 64, device=DEV)
+    am = word(1.0)
+    ep = K.Epilogue(K.ptr(y), None, None, None, K.EP_PLAIN, 0)
+    with pytest.raises(K.SelunetError):  # below the halo tile
+        K.call("selunet_conv3x3_x2", K.gather(n, h, w, 9, K.source(x, c)), K.ptr(u), 64, ep, K.ptr(am), None,
+               K.stream_ptr())
+    h = w = 16
+    x = torch.zeros(n * h * w, c, device=DEV)
+    y = torch.empty(n * h * w, 64, device=DEV)
+    ep = K.Epilogue(K.ptr(y), None, None, None, K.EP_PLAIN, 0)
+    with pytest.raises(K.SelunetError):  # no range word
+        K.call("selunet_conv3x3_x2", K.gather(n, h, w, 9, K.source(x, c)), K.ptr(u), 64, ep, None, None,
+               K.stream_ptr())
+
+
+def test_act_bound():
+    """Samuelson: |xhat| <= sqrt(count - 1) under batch statistics, so the word bounds relu(bn(y))."""
+    c, count = 96, 5000
+    gamma, beta = gen(c, seed=1).to(DEV), gen(c, seed=2).to(DEV)
+    out = torch.empty(1, device=DEV)
+    K.call("selunet_act_bound", K.ptr(gamma), K.ptr(beta), c, count, K.ptr(out), K.stream_ptr())
+    want = gamma.abs().max().item() * count ** 0.5 + beta.abs().max().item()
+    assert abs(out.item() - want) <= 2e-4 * want
+    # an adversarial batch: one outlier per channel reaches the bound's sqrt(count - 1) * sigma
+    y = torch.zeros(count, c, dtype=torch.float64)
+    y[0] = 1.0
+    xhat = (y - y.mean(0)) / y.std(0, unbiased=False)
+    a = (xhat * gamma.cpu().double() + beta.cpu().double()).abs().max().item()
+    assert a <= out.item()
+
+
+def test_bn_bwd_apply_amax_and_epilogue_amax():
+    m, c = 4096, 64
+    dz, y = gen(m, c, seed=1).to(DEV), gen(m, c, seed=2).to(DEV)
+    sc, sh = (gen(c, seed=3).abs() + 0.5).to(DEV), gen(c, seed=4).to(DEV)
+    mean, invstd = (gen(c, seed=5) * 0.1).to(DEV), (gen(c, seed=6).abs() + 0.5).to(DEV)
+    coef = gen(3, c, seed=7).to(DEV) * 1e-3
+    dy, dy2 = torch.empty(m, c, device=DEV), torch.empty(m, c, device=DEV)
+    am = torch.zeros(1, device=DEV)
+    args = [K.ptr(t) for t in (dz, y)] + [m, c] + [K.ptr(t) for t in (sc, sh, mean, invstd, coef)]
+    K.call("selunet_bn_bwd_apply", *args, K.ptr(dy), K.F32, K.stream_ptr())
+    K.call("selunet_bn_bwd_apply_amax", *args, K.ptr(dy2), K.ptr(am), K.F32, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dy, dy2) and am.item() == dy.abs().max().item()
+    # ConvTranspose2d forward (SCATTER2X) with the output range word
+    n, h, w, ci, co = 2, 8, 8, 64, 32
+    x = gen(n * h * w, ci, seed=8).to(DEV)
+    wp = gen(4 * co, ci, seed=9, scale=0.1).to(DEV)
+    bias = gen(co, seed=10).to(DEV)
+    up = torch.empty(n * 4 * h * w, co, device=DEV)
+    am2 = torch.zeros(1, device=DEV)
+    ep = K.Epilogue(K.ptr(up), None, K.ptr(bias), None, K.EP_SCATTER2X, 0)
+    ep.amax = K.ptr(am2)
+    K.call("selunet_gemm_gather", K.gather(n, h, w, 1, K.source(x, ci)), K.ptr(wp), 4 * co, ci, ep, K.F32,
+           K.stream_ptr())
+    torch.cuda.synchronize()
+    assert am2.item() == up.abs().max().item()
