@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="fp32", help="headline configuration")
     ap.add_argument("--no-bf16", action="store_true", help="skip the extra bf16 measurement")
+    ap.add_argument("--no-exact", action="store_true", help="skip the extra exact-fp32-MFMA measurement")
     ap.add_argument("--selective", type=int, default=1, help="0: non-selective UNet_B (BASELINE configs[1])")
     ap.add_argument("--lamb", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -82,9 +83,10 @@ class KernelTimer:
     dispatches to, with its algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM) and algorithmic
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
-    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws",
-            "selunet_gemm_wgrad_ws_to")
-    HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_maxpool2_fwd",
+    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_conv3x3_x2", "selunet_gemm_wgrad",
+            "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
+    HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
+           "selunet_maxpool2_fwd",
            "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
 
     def __init__(self, esz, tag):
@@ -123,6 +125,15 @@ class KernelTimer:
             flops = 2.0 * m * n_cols * 6 * c
             nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * 12 * c * esz
             return kname, "mfma", flops, nbytes, f"wino {g.h}x{g.w} C={c} N={n_cols} mode={ep.mode}"
+        if name == "selunet_conv3x3_x2":  # (g, w, n_cols, ep, amax0, amax1, stream): split-fp16 fp32 conv
+            g, n_cols, ep = args[0], _i(args[2]), args[3]
+            kname = K.query("selunet_conv3x3_x2_kernel_name", n_cols, ep.mode, ep.split).decode()
+            m = g.n * g.h * g.w
+            # the fp16 MFMA work executed: three products (hh, hl, lh) per fp32 product, against the
+            # fp16 dense peak ("mfma_f16")
+            flops = 3 * 2.0 * m * n_cols * self._k(g)
+            nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
+            return kname, "mfma_f16", flops, nbytes, f"x2 {g.h}x{g.w} K={self._k(g)} N={n_cols} mode={ep.mode}"
         if name in ("selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to"):
             gp, gq = args[0], args[1]
             dt = _i(args[{"selunet_gemm_wgrad": 3, "selunet_gemm_wgrad_ws": 5, "selunet_gemm_wgrad_ws_to": 7}[name]])
@@ -144,7 +155,7 @@ class KernelTimer:
             m = n * h * w
             return (f"first_conv_wgrad<{t}>", "hbm", 2.0 * m * 64 * 9 * cin, m * cin * 4 + m * 64 * esz,
                     f"first wgrad {h}x{w}")
-        if name == "selunet_bn_bwd_apply":  # (dA, y, M, C, ...): read dA + y, write dy
+        if name in ("selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax"):  # (dA, y, M, C, ...): read dA + y, write dy
             m, c = _i(args[2]), _i(args[3])
             return f"bn_bwd_apply<{t}>", "hbm", 0.0, 3 * m * c * esz, f"bn_bwd_apply C={c}"
         if name == "selunet_maxpool2_fwd":  # (y, n, h, w, c, ...): read y, write y/4
@@ -349,9 +360,9 @@ def roofline(args, dtype, timer, ksteps, kel, local_batch):
     def frac(v):
         if v["ms"] <= 0:
             return 0.0, 0.0
-        if v["bound"] == "mfma":
+        if v["bound"] in ("mfma", "mfma_f16"):
             a = v["flops"] / (v["ms"] * 1e-3) / 1e12
-            return a, a / mfma_peak
+            return a, a / (PEAK["bf16"][0] if v["bound"] == "mfma_f16" else mfma_peak)
         a = v["bytes"] / (v["ms"] * 1e-3) / 1e9
         return a, a / HBM_PEAK_GBS
 
@@ -362,9 +373,13 @@ def roofline(args, dtype, timer, ksteps, kel, local_batch):
     # the committed PMC summary was collected on the default workload (bs=128 per GPU, 256x256)
     traffic, tsrc = load_traffic(dom) if (args.size, local_batch) == (256, 128) else (None, None)
     hbm = d["bound"] == "hbm"
+    f16 = d["bound"] == "mfma_f16"
     return {
-        "bound": d["bound"], "kernel": dom, "achieved": round(achieved, 2),
-        "peak": HBM_PEAK_GBS if hbm else mfma_peak, "unit": "GB/s" if hbm else mfma_unit, "frac": round(fr, 4),
+        "bound": "mfma" if f16 else d["bound"], "kernel": dom, "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS if hbm else (PEAK["bf16"][0] if f16 else mfma_peak),
+        "unit": "GB/s" if hbm else mfma_unit, "frac": round(fr, 4),
+        "peak_basis": "fp16 dense MFMA peak; achieved counts the three fp16 products per fp32 product the "
+                      "split-fp16 kernel executes" if f16 else None,
         "traffic": traffic["hbm_bytes_per_launch"] if traffic else None, "traffic_source": tsrc,
         "algorithmic_flops_per_launch": d["flops"] / launches, "algorithmic_bytes_per_launch": d["bytes"] / launches,
         "per_launch_ms": round(d["ms"] / launches, 4), "launches": d["launches"],
@@ -399,7 +414,14 @@ def main():
     del x, lab
 
     head = run_config(args, args.dtype, world, rank, dev, xt, lt, hi - lo)
-    extra = None
+    extra = exact = None
+    if args.dtype == "fp32" and not args.no_exact and world == 1:
+        # the same fp32 step on the exact-fp32-MFMA kernels (Winograd / direct), for comparison
+        os.environ["SELUNET_X2"] = "0"
+        try:
+            exact = run_config(args, "fp32", world, rank, dev, xt, lt, hi - lo)
+        finally:
+            os.environ.pop("SELUNET_X2", None)
     if args.dtype == "fp32" and not args.no_bf16:
         extra = run_config(args, "bf16", world, rank, dev, xt, lt, hi - lo)
 
@@ -421,17 +443,25 @@ def main():
                                    f"Adam lr=1e-3" + (f", s_lamb={args.lamb:g}" if args.selective else ""),
                        "model": model, "global_batch": args.batch, "per_gpu_batch": hi - lo, "image": args.size,
                        "parallelism": f"dp{world}",
-                       "arithmetic": "fp32 operands, exact fp32 MFMA products, fp32 accumulation; 3x3 forward and "
-                                     "data-gradient convolutions as 1-D Winograd F(2,3) with fp32 transforms"
+                       "arithmetic": "fp32 tensors and accumulation; 3x3 forward and data-gradient convolutions "
+                                     "on split-fp16 operands (each fp32 operand scaled by a power of two and "
+                                     "split into fp16 high + low parts, 22 significant bits; three fp16 MFMA "
+                                     "products per fp32 product; error vs fp64 at or below the exact fp32 MFMA's, "
+                                     "tools/split_probe.hip); weight gradients as fp32 1-D Winograd F(2,3) on "
+                                     "exact fp32 MFMAs"
                        if args.dtype == "fp32" else "bf16 operands, fp32 accumulation"},
             "gpu": torch.cuda.get_device_name(dev),
             "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
-            "step_flops_basis": "direct-convolution FLOPs of the training step (the fp32 Winograd layers execute "
-                                "2/3 of their share)" if args.dtype == "fp32" else "direct-convolution FLOPs",
+            "step_flops_basis": "direct-convolution FLOPs of the training step (the fp32 Winograd weight gradients "
+                                "execute 2/3 of their share)" if args.dtype == "fp32" else "direct-convolution FLOPs",
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
             "full_loop": head.get("full_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,
         }
+        if exact is not None:
+            exact["note"] = ("the same fp32 step with every convolution on exact fp32 MFMA products (1-D Winograd "
+                             "F(2,3) forward / data-gradient / weight-gradient kernels; SELUNET_X2=0)")
+            line["exact_f32"] = exact
         if extra is not None:
             wb = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * extra["value"] / 1e3
             extra["step_tflops"] = round(wb, 2)

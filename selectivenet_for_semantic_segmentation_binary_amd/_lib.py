@@ -520,8 +520,12 @@ def dtype_code(dt: torch.dtype) -> int:
     raise ValueError(f"unsupported activation dtype {dt}")
 
 
-def source(data, channels, scale=None, shift=None, relu=True, layout=0) -> Source:
-    return Source(ptr(data), ptr(scale), ptr(shift), channels, int(bool(relu) and scale is not None), layout, 0)
+def source(data, channels, scale=None, shift=None, relu=True, layout=0, amax=None) -> Source:
+    """A gather source; amax (a 1-element fp32 device tensor, optional) is the range word of the
+    source's values after its transform, kept on the Python object for selunet_conv3x3_x2."""
+    s = Source(ptr(data), ptr(scale), ptr(shift), channels, int(bool(relu) and scale is not None), layout, 0)
+    s.amax = amax
+    return s
 
 
 def gather(n, h, w, taps, *srcs: Source) -> Gather:

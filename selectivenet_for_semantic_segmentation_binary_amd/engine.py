@@ -43,9 +43,22 @@ class BNState:
     h: int
     w: int
     c: int
+    amax: torch.Tensor = None  # range word of relu(bn(y)) (split-fp16 layers, selunet_act_bound)
 
     def src(self):
-        return K.source(self.y, self.c, self.scale, self.shift, relu=True)
+        return K.source(self.y, self.c, self.scale, self.shift, relu=True, amax=self.amax)
+
+
+@dataclass
+class WPack:
+    """A conv layer's weight operands for the step: fwd / dgrad packs, the forward's K, output
+    channels, and the kernel form: "direct" (halo / gather GEMM in the compute dtype), "wino" (fp32
+    Winograd F(2,3)) or "x2" (fp32 on split-fp16 operands, selunet_conv3x3_x2)."""
+    fwd: torch.Tensor
+    dgrad: torch.Tensor
+    kpad: int
+    co: int
+    mode: str = "direct"
 
 
 @dataclass
@@ -74,6 +87,8 @@ class Ctx:
     pools: dict = field(default_factory=dict)
     ups: dict = field(default_factory=dict)
     wpack: dict = field(default_factory=dict)
+    words: dict = field(default_factory=dict)  # operand range words (split-fp16 layers) by key
+    x2: bool = False                           # some layer of this pass runs split-fp16
 
 
 class _Entry:
@@ -108,6 +123,9 @@ class Engine:
         self.bke = 128 // torch.empty((), dtype=dt).element_size()
         self.plans_enabled = os.environ.get("SELUNET_NO_PLANS", "0") != "1"
         self.deterministic = os.environ.get("SELUNET_DETERMINISTIC", "1") != "0"
+        # fp32 training: 3x3 layers on split-fp16 operands (selunet_conv3x3_x2); SELUNET_X2=0 keeps
+        # the exact-fp32-MFMA kernels (Winograd / direct)
+        self.x2 = dt == torch.float32 and os.environ.get("SELUNET_X2", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -157,56 +175,89 @@ class Engine:
         else:
             K.call("selunet_unpack_convT_grad", K.ptr(packed), ni, out.shape[1], K.ptr(out), self.stream)
 
+    @staticmethod
+    def _layer_hw(name, hw):
+        f = 1 << (int(name.split("_")[2]) - 1)  # encoder/decoder level k runs at 1 / 2^(k-1)
+        return hw[0] // f, hw[1] // f
+
+    @staticmethod
+    def _concat_c0(name, ci):
+        concat = name.startswith("decoder_layer") and name.endswith("_2") and name != "decoder_layer_4_2"
+        return ci // 2 if concat else ci  # torch.cat((unpool, skip)) inputs: two equal sources
+
+    def _shape_ok(self, query, name, ci, co, hw, need_dgrad):
+        h, w = self._layer_hw(name, hw)
+        ok = K.query(query, h, w, ci, self._concat_c0(name, ci), co) == 1
+        return ok and (not need_dgrad or K.query(query, h, w, co, co, ci) == 1)
+
     def _wino_ok(self, name, ci, co, hw, need_dgrad):
         """fp32 layers whose forward (and data gradient) run as the Winograd F(2,3) kernel
         (selunet_conv3x3_wino): decided from the layer's resolution and channels."""
         if self.dt != torch.float32 or hw is None or name == "encoder_layer_1_1":
             return False
-        f = 1 << (int(name.split("_")[2]) - 1)  # encoder/decoder level k runs at 1 / 2^(k-1)
-        h, w = hw[0] // f, hw[1] // f
-        concat = name.startswith("decoder_layer") and name.endswith("_2") and name != "decoder_layer_4_2"
-        c0 = ci // 2 if concat else ci  # torch.cat((unpool, skip)) inputs: two equal sources
-        ok = K.query("selunet_conv3x3_wino_ok", h, w, ci, c0, co) == 1
-        return ok and (not need_dgrad or K.query("selunet_conv3x3_wino_ok", h, w, co, co, ci) == 1)
+        return self._shape_ok("selunet_conv3x3_wino_ok", name, ci, co, hw, need_dgrad)
 
-    def pack_weights(self, P, need_dgrad=True, hw=None):
+    def _x2_ok(self, name, ci, co, hw, need_dgrad, training):
+        """fp32 training layers on split-fp16 operands (selunet_conv3x3_x2). Training only: the range
+        word of a BN+ReLU input (selunet_act_bound) holds for batch statistics."""
+        if not (self.x2 and training) or hw is None or name == "encoder_layer_1_1":
+            return False
+        return self._shape_ok("selunet_conv3x3_x2_ok", name, ci, co, hw, need_dgrad)
+
+    def pack_weights(self, P, need_dgrad=True, hw=None, training=False):
         """fp32 master weights -> GEMM operand layouts in the compute dtype (one launch for all);
-        fp32 layers at input resolution hw that the Winograd kernel takes get its U operands.
-        Returns name -> (fwd, dgrad, k_pad or ci, winograd)."""
+        fp32 layers at input resolution hw get the split-fp16 (training) or Winograd operands.
+        Returns name -> WPack."""
         dev = P["encoder_layer_1_2.0.weight"].device
         packs = {}
         pl = K.PackList()
         for name, ci, co in LY.CBR_LAYERS:
             w = P[f"{name}.0.weight"]
             ci = w.shape[1]
-            wino = self._wino_ok(name, ci, co, hw, need_dgrad)
-            if wino:
-                kpad, taps, kind = 12 * ci, 12, K.PACK_CONV3X3_WINO
-            else:
-                kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
-                taps, kind = 9, K.PACK_CONV3X3
-            fwd = K.keep(torch.empty(co, kpad, dtype=self.dt, device=dev))
             dg = None
-            if need_dgrad and name != "encoder_layer_1_1":
-                dg = K.keep(torch.empty(ci, taps * co, dtype=self.dt, device=dev))
+            if self._x2_ok(name, ci, co, hw, need_dgrad, training):
+                mode, kpad, kind = "x2", 9 * ci, K.PACK_CONV3X3_X2
+                fwd = K.keep(torch.empty(co * kpad + co, dtype=torch.float32, device=dev))
+                if need_dgrad:
+                    dg = K.keep(torch.empty(ci * 9 * co + ci, dtype=torch.float32, device=dev))
+            else:
+                if self._wino_ok(name, ci, co, hw, need_dgrad):
+                    mode, kpad, taps, kind = "wino", 12 * ci, 12, K.PACK_CONV3X3_WINO
+                else:
+                    kpad = FIRST_KPAD if name == "encoder_layer_1_1" else _rup(9 * ci, self.bke)
+                    mode, taps, kind = "direct", 9, K.PACK_CONV3X3
+                fwd = K.keep(torch.empty(co, kpad, dtype=self.dt, device=dev))
+                if need_dgrad and name != "encoder_layer_1_1":
+                    dg = K.keep(torch.empty(ci, taps * co, dtype=self.dt, device=dev))
             pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), kind, co, ci, kpad, 0)
             pl.n += 1
-            packs[name] = (fwd, dg, kpad, wino)
+            packs[name] = WPack(fwd, dg, kpad, co, mode)
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
             fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
             dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
             pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
             pl.n += 1
-            packs[name] = (fwd, dg, ci, False)
+            packs[name] = WPack(fwd, dg, ci, co)
         K.call("selunet_pack_weights", pl, self.code, self.stream)
         return packs
 
+    def _word(self, ctx, key):
+        """The range word `key` of this forward/backward (zeroed at the start of the forward)."""
+        return ctx.words[key]
+
     # ------------------------------------------------------------------ forward pieces
-    def _conv3x3(self, g, b, n_cols, kpad, ep, wino):
+    def _conv3x3(self, g, b, n_cols, kpad, ep, mode, srcs=()):
         """A 3x3 conv (forward or data gradient) through the direct halo / gather kernels, or the
-        fp32 Winograd kernel when the layer's operands were packed for it."""
-        if wino:
+        fp32 Winograd / split-fp16 kernel when the layer's operands were packed for it (srcs: the
+        gather's sources, whose range words the split-fp16 kernel reads)."""
+        if mode == "x2":
+            words = [s.amax for s in srcs]
+            if any(wd is None for wd in words):
+                raise RuntimeError("split-fp16 conv: a source without its range word")
+            K.call("selunet_conv3x3_x2", g, K.ptr(b), n_cols, ep, K.ptr(words[0]),
+                   K.ptr(words[1]) if len(words) > 1 else None, self.stream)
+        elif mode == "wino":
             K.call("selunet_conv3x3_wino", g, K.ptr(b), n_cols, ep, self.stream)
         else:
             K.call("selunet_gemm_gather", g, K.ptr(b), n_cols, kpad, ep, self.code, self.stream)
@@ -214,8 +265,8 @@ class Engine:
     def _cbr(self, ctx, name, P, B, n, h, w, *srcs, taps=9, first_x=None):
         """CBR_2D forward (model.py:9-15): conv (+ BN batch statistics in its epilogue), BN finalize.
         first_x: the network input (NCHW fp32) for encoder_layer_1_1, convolved directly."""
-        fwd, _, kpad, wino = ctx.wpack[name]
-        co = fwd.shape[0]
+        wp = ctx.wpack[name]
+        fwd, kpad, co = wp.fwd, wp.kpad, wp.co
         M = n * h * w
         dev = fwd.device
         y = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
@@ -232,7 +283,7 @@ class Engine:
                    K.ptr(stats), self.code, self.stream)
         else:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
-            self._conv3x3(g, fwd, co, kpad, ep, wino)
+            self._conv3x3(g, fwd, co, kpad, ep, wp.mode, srcs)
         mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
         if ctx.training and self.dt == torch.float32:
             # fp32 (parity): two-pass statistics — the epilogue's sums give the batch mean, a second
@@ -264,6 +315,10 @@ class Engine:
                    K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, 0,
                    K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
         st = BNState(y, mean, invstd, scale, shift, n, h, w, co)
+        if ctx.x2:  # range word of relu(bn(y)) for the split-fp16 consumers (batch statistics)
+            st.amax = self._word(ctx, "act:" + name)
+            K.call("selunet_act_bound", K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]), co, M,
+                   K.ptr(st.amax), self.stream)
         ctx.bn[name] = st
         return st
 
@@ -275,11 +330,13 @@ class Engine:
         return out
 
     def _up(self, ctx, name, P, st: BNState):
-        fwd, _, ci, _ = ctx.wpack[name]
-        co = fwd.shape[0] // 4
+        wp = ctx.wpack[name]
+        fwd, ci, co = wp.fwd, wp.kpad, wp.co
         out = K.keep(torch.empty(st.n * 2 * st.h * 2 * st.w, co, dtype=self.dt, device=st.y.device))
         g = K.gather(st.n, st.h, st.w, 1, st.src())
         ep = K.Epilogue(K.ptr(out), None, K.ptr(P[f"{name}.bias"]), None, K.EP_SCATTER2X, 0)
+        if ctx.x2:  # range word of the up-sampled tensor (exact max, the epilogue's atomic)
+            ep.amax = K.ptr(self._word(ctx, "up:" + name))
         K.call("selunet_gemm_gather", g, K.ptr(fwd), 4 * co, ci, ep, self.code, self.stream)
         ctx.ups[name] = out
         return out
@@ -353,29 +410,38 @@ class Engine:
         n, cin, H, W = x.shape
         ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
         ctx.ce_heads = ce_heads
-        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W))
+        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W), training=training)
+        ctx.x2 = any(wp.mode == "x2" for wp in ctx.wpack.values())
+        if ctx.x2:  # the operand range words of this step, zeroed for their atomic-max producers
+            keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy")]
+            keys += ["up:" + nm for nm, _, _ in LY.UNPOOLS]
+            buf = K.keep(torch.empty(len(keys), dtype=torch.float32, device=x.device))
+            K.call("selunet_memset", K.ptr(buf), 0, buf.numel() * 4, self.stream)
+            ctx.words = {k: buf[i:i + 1] for i, k in enumerate(keys)}
         c = lambda name, h, w, *s: self._cbr(ctx, name, P, B, n, h, w, *s)  # noqa: E731
         h1, w1, h2, w2, h3, w3, h4, w4 = H, W, H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
         # first layer (C_in = 3 or 2): convolved straight from the NCHW fp32 input
         e11 = self._cbr(ctx, "encoder_layer_1_1", P, B, n, h1, w1, first_x=x)
         e12 = c("encoder_layer_1_2", h1, w1, e11.src())
         p1 = self._pool(ctx, "pool1", e12)
-        e21 = c("encoder_layer_2_1", h2, w2, K.source(p1, 64))
+        wd = lambda st: st.amax  # noqa: E731  a pooled copy keeps its source's range
+        e21 = c("encoder_layer_2_1", h2, w2, K.source(p1, 64, amax=wd(e12)))
         e22 = c("encoder_layer_2_2", h2, w2, e21.src())
         p2 = self._pool(ctx, "pool2", e22)
-        e31 = c("encoder_layer_3_1", h3, w3, K.source(p2, 128))
+        e31 = c("encoder_layer_3_1", h3, w3, K.source(p2, 128, amax=wd(e22)))
         e32 = c("encoder_layer_3_2", h3, w3, e31.src())
         p3 = self._pool(ctx, "pool3", e32)
-        b42 = c("decoder_layer_4_2", h4, w4, K.source(p3, 256))
+        b42 = c("decoder_layer_4_2", h4, w4, K.source(p3, 256, amax=wd(e32)))
         b41 = c("decoder_layer_4_1", h4, w4, b42.src())
         u3 = self._up(ctx, "unpool3", P, b41)
-        d32 = c("decoder_layer_3_2", h3, w3, K.source(u3, 256), e32.src())
+        uw = lambda nm: ctx.words.get("up:" + nm)  # noqa: E731
+        d32 = c("decoder_layer_3_2", h3, w3, K.source(u3, 256, amax=uw("unpool3")), e32.src())
         d31 = c("decoder_layer_3_1", h3, w3, d32.src())
         u2 = self._up(ctx, "unpool2", P, d31)
-        d22 = c("decoder_layer_2_2", h2, w2, K.source(u2, 128), e22.src())
+        d22 = c("decoder_layer_2_2", h2, w2, K.source(u2, 128, amax=uw("unpool2")), e22.src())
         d21 = c("decoder_layer_2_1", h2, w2, d22.src())
         u1 = self._up(ctx, "unpool1", P, d21)
-        d12 = c("decoder_layer_1_2", h1, w1, K.source(u1, 64), e12.src())
+        d12 = c("decoder_layer_1_2", h1, w1, K.source(u1, 64, amax=uw("unpool1")), e12.src())
         d11 = c("decoder_layer_1_1", h1, w1, d12.src())
         M = n * H * W
         if ce_heads is not None:
@@ -444,8 +510,14 @@ class Engine:
                K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]),
                K.ptr(coef), self.stream)
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
-        K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
-               K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
+        wp = ctx.wpack[name]
+        dyw = self._word(ctx, "dy:" + name) if wp.mode == "x2" else None
+        if dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
+            K.call("selunet_bn_bwd_apply_amax", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+                   K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.code, self.stream)
+        else:
+            K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+                   K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
         if first_x is not None:
             cin = first_x.shape[1]
@@ -467,8 +539,9 @@ class Engine:
         K.marker(("grads", name))
         if not need_dgrad:
             return None
-        _, wd, _, wino = ctx.wpack[name]
-        ga = K.gather(st.n, st.h, st.w, 9, K.source(dy, co))
+        wd = wp.dgrad
+        dsrc = K.source(dy, co, amax=dyw)
+        ga = K.gather(st.n, st.h, st.w, 9, dsrc)
         rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
         if dgrad_split is None:
             dx = K.keep(torch.empty(M, ci, dtype=self.dt, device=dev))
@@ -477,21 +550,21 @@ class Engine:
             if prev is not None:
                 slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
                 ep.bnb = bnb_for(prev, slab)
-            self._conv3x3(ga, wd, ci, 9 * co, ep, wino)
+            self._conv3x3(ga, wd, ci, 9 * co, ep, wp.mode, (dsrc,))
             return DGrad(dx, slab, rows)
         c0 = dgrad_split
         d0 = K.keep(torch.empty(M, c0, dtype=self.dt, device=dev))
         d1 = K.keep(torch.empty(M, ci - c0, dtype=self.dt, device=dev))
         colsum = K.keep(torch.empty(rows, c0, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0, K.ptr(colsum))
-        self._conv3x3(ga, wd, ci, 9 * co, ep, wino)
+        self._conv3x3(ga, wd, ci, 9 * co, ep, wp.mode, (dsrc,))
         return DGrad(d0, colsum, rows), d1
 
     def _up_bwd(self, ctx, name, du: DGrad, G, prev: BNState):
         """ConvTranspose2d(k2,s2) backward: bias (from du's column sums), weight and data gradients;
         the data gradient carries prev's BN-backward sums."""
-        fwd, wd, ci, _ = ctx.wpack[name]
-        co = fwd.shape[0] // 4
+        wp = ctx.wpack[name]
+        wd, ci, co = wp.dgrad, wp.kpad, wp.co
         n, h, w = prev.n, prev.h, prev.w
         dev = du.t.device
         self._reduce(du.slab, du.rows, co, out32=G[f"{name}.bias"])

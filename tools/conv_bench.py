@@ -1,7 +1,7 @@
 """Per-layer timing of the 3x3 conv kernels at the bench shapes (bs=128) — profiling tool.
 
     python tools/conv_bench.py [--batch 128] [--iters 20] [--only fwd|dgrad|wgrad] [--layers enc1_2,dec1_2]
-                               [--dtype bf16|fp32] [--wino]
+                               [--dtype bf16|fp32] [--wino | --x2]
 
 Calls selunet_gemm_gather directly on random NHWC operands (forward: BN+ReLU transform of the
 producer applied on load, BN-stat epilogue; dgrad: untransformed dY, the SPLIT epilogue where the
@@ -27,7 +27,7 @@ LAYERS = [
 ]
 
 
-def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False):
+def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False, x2=False):
     dev = "cuda"
     srcs = []
     keep = []
@@ -58,8 +58,17 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
     if wino:  # fp32 Winograd F(2,3): U = [co][12*ci] (random values: timing only)
         w = torch.randn(co, 12 * ci, device=dev) * 0.05
         name = K.query("selunet_conv3x3_wino_kernel_name", co, ep.mode, ep.split).decode()
+    if x2:  # fp32 on split-fp16 operands: [co][9*ci] words + co unscale factors (random: timing only)
+        w = torch.randn(co * kp + co, device=dev).abs() * 1e-3 + 1e-3
+        amax = torch.full((1,), 8.0, device=dev)
+        keep.append(amax)
+        name = K.query("selunet_conv3x3_x2_kernel_name", co, ep.mode, ep.split).decode()
 
     def call():
+        if x2:
+            K.call("selunet_conv3x3_x2", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.ptr(amax), K.ptr(amax),
+                   K.stream_ptr())
+            return
         if wino:
             K.call("selunet_conv3x3_wino", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.stream_ptr())
             return
@@ -129,6 +138,7 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--wino", action="store_true", help="fp32 Winograd F(2,3) kernel (direct-conv FLOPs reported)")
+    ap.add_argument("--x2", action="store_true", help="fp32 on split-fp16 operands (selunet_conv3x3_x2)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     sel = set(a.layers.split(",")) if a.layers else None
@@ -137,7 +147,7 @@ def main():
         if sel and name not in sel:
             continue
         if a.only not in ("dgrad", "wgrad"):
-            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino)
+            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino, a.x2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
@@ -148,7 +158,7 @@ def main():
             print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
             continue
         if a.only != "fwd":
-            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino)
+            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino, a.x2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"dgrad {name:8s} {co:4d}->{c0 + c1:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
