@@ -83,8 +83,8 @@ class KernelTimer:
     dispatches to, with its algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM) and algorithmic
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
-    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_conv3x3_x2", "selunet_gemm_wgrad",
-            "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
+    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_conv3x3_x2", "selunet_conv3x3_wgrad_x2",
+            "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
            "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
@@ -134,6 +134,12 @@ class KernelTimer:
             flops = 3 * 2.0 * m * n_cols * self._k(g)
             nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
             return kname, "mfma_f16", flops, nbytes, f"x2 {g.h}x{g.w} K={self._k(g)} N={n_cols} mode={ep.mode}"
+        if name == "selunet_conv3x3_wgrad_x2":  # (gp, gq, ws, wsb, out, amax_p, amax_q0, amax_q1, stream)
+            gp, gq = args[0], args[1]
+            kname = f"conv3x3_wgrad_x2<{128 if self._k(gp) % 128 == 0 else 64}>+reduce"
+            flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work
+            nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
+            return kname, "mfma_f16", flops, nbytes, f"wgrad x2 {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
         if name in ("selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to"):
             gp, gq = args[0], args[1]
             dt = _i(args[{"selunet_gemm_wgrad": 3, "selunet_gemm_wgrad_ws": 5, "selunet_gemm_wgrad_ws_to": 7}[name]])
@@ -447,13 +453,11 @@ def main():
                                      "on split-fp16 operands (each fp32 operand scaled by a power of two and "
                                      "split into fp16 high + low parts, 22 significant bits; three fp16 MFMA "
                                      "products per fp32 product; error vs fp64 at or below the exact fp32 MFMA's, "
-                                     "tools/split_probe.hip); weight gradients as fp32 1-D Winograd F(2,3) on "
-                                     "exact fp32 MFMAs"
+                                     "tools/split_probe.hip), weight gradients likewise"
                        if args.dtype == "fp32" else "bf16 operands, fp32 accumulation"},
             "gpu": torch.cuda.get_device_name(dev),
             "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
-            "step_flops_basis": "direct-convolution FLOPs of the training step (the fp32 Winograd weight gradients "
-                                "execute 2/3 of their share)" if args.dtype == "fp32" else "direct-convolution FLOPs",
+            "step_flops_basis": "direct-convolution FLOPs of the training step",
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
             "full_loop": head.get("full_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,

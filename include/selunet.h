@@ -153,6 +153,16 @@ const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32
  * epilogues and statistics slab rows as selunet_gemm_gather; selunet_conv3x3_x2_ok tells whether a
  * layer can take it (h, w >= 16, C and c_src0 multiples of 32, C > 32, n_cols a multiple of 64). */
 int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
+/* fp32 3x3 weight gradient (autograd of model.py:11's weight) on split-fp16 operands, the same
+ * arithmetic as selunet_conv3x3_x2: p = dY (1 tap, [M][co]), q = the layer input (3x3 gather, BN+ReLU
+ * transforms of its sources); amax_p / amax_q0 / amax_q1 their range words. Pixel-split partials in
+ * ws (>= selunet_conv3x3_wgrad_x2_ws_bytes) are summed in a fixed order straight into out, the
+ * Conv2d weight layout [co][ci][3][3] (deterministic). -1 bytes: operands not eligible (q: h >= 8,
+ * w >= 16, channels multiples of 64; co a multiple of 64). */
+int64_t selunet_conv3x3_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q);
+int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                             float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                             void* stream);
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split);

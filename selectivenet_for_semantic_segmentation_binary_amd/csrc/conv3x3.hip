@@ -1211,6 +1211,253 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
   }
 }
 
+// =========================================================================== split-fp16 weight gradient
+// fp32 3x3 weight gradient on split-fp16 operands (selunet_conv3x3_wgrad_x2): the bf16 halo kernel's
+// structure (MFMA k = pixel, both operands read with ds_read_b64_tr_b16 from their natural
+// [pixel][channel] tiles, one dY fragment feeding every tap of the wave) with each operand staged as
+// two fp16 planes, h = fp16(v * 2^e) and l = fp16(v * 2^e - h), and three v_mfma_f32_32x32x16_f16
+// per tap and k-step (hl, lh, hh). 8 x 8-pixel tiles (10 x 10 halo) so that both planes of both
+// operands double-buffer in LDS (BI = 128: 155 KB). The partials are unscaled by 2^-(e_dy + e_x)
+// (one source per 64-channel chunk, so one scale per workgroup) and reduced like the halo kernels'.
+constexpr int XTH = 8, XTW = 8, XHW = XTW + 2, XHP = (XTH + 2) * XHW, XPIX = XTH * XTW;
+
+template <int BI>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_chunks, int64_t tiles_per_split,
+                        int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
+                        const float* __restrict__ amax_p, const float* __restrict__ amax_q0,
+                        const float* __restrict__ amax_q1) {
+  constexpr int LDP = BI + 32;                   // dY plane row stride (halves): 16 dwords mod 64
+  constexpr int LDX = 64 + 32;                   // halo plane row stride (halves)
+  constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
+  constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
+  constexpr int P_ROUNDS = (XPIX * BI / 4) / 512;
+  constexpr int X_ROUNDS = (XHP * 16 + 511) / 512;
+  static_assert(P_ROUNDS * 512 == XPIX * BI / 4, "dY tile must split evenly over the threads");
+
+  __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][XPIX][LDP];  // [buffer][h, l][pixel][co]
+  __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][XHP][LDX];   // [buffer][h, l][halo pixel][ci]
+  __shared__ float Ks[2 * BI + 2 * 64];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wj = wave & 1;                       // ci subtile
+  const int wi = (wave >> 1) % (BI / 32);        // co subtile
+  const int tg = (wave >> 1) / (BI / 32);        // tap group
+  const int tap0 = tg * 5;
+  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
+  const int half = lane >> 5, l32 = lane & 31;
+  const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int cot = lb % co_tiles;
+  const int rest = lb / co_tiles;
+  const int cik = rest % ci_chunks;
+  const int64_t split = rest / ci_chunks;
+  const int i0 = cot * BI;
+  const int c0 = cik * 64;
+  const int64_t pt_begin = split * tiles_per_split;
+  const int64_t pt_end = min(total_tiles, pt_begin + tiles_per_split);
+
+  int xs_src = 0, xc = c0;
+  if (Q.nsrc > 1 && xc >= Q.src[0].C) {
+    xc -= Q.src[0].C;
+    xs_src = 1;
+  }
+  const SrcArg xa = pick_src(Q, xs_src);
+  const SrcArg& pa = P.src[0];
+  const int H = P.h, W = P.w;
+  float uns_p, uns_x;
+  const float sp = x2_scale(amax_p[0], &uns_p);
+  const float sx = x2_scale((xs_src ? amax_q1 : amax_q0)[0], &uns_x);
+
+  if (tid < 2 * BI + 128) {
+    float v;
+    if (tid < 2 * BI) {
+      const int c = i0 + (tid % BI);
+      v = pa.scale ? (tid < BI ? pa.scale[c] : pa.shift[c]) : 0.0f;
+    } else {
+      const int c = xc + ((tid - 2 * BI) % 64);
+      v = xa.scale ? (tid < 2 * BI + 64 ? xa.scale[c] : xa.shift[c]) : 0.0f;
+    }
+    Ks[tid] = v;
+  }
+
+  auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
+    x0 = ((unsigned)pt - r2 * (unsigned)tiles_x) * XTW;
+    const unsigned r3 = r2 / (unsigned)tiles_y;
+    y0 = (r2 - r3 * (unsigned)tiles_y) * XTH;
+    img = (int)r3;
+  };
+  // 4 fp32 channels -> (BN+ReLU) -> scale -> h / l fp16 quads at plane rows hp / lp
+  auto put = [&](float4 v, const float* sc, const float* sh, int relu, float s, _Float16* hp, _Float16* lp)
+      __attribute__((always_inline)) {
+    float f[4] = {v.x, v.y, v.z, v.w};
+    f16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = f[j];
+      if (sc) {
+        t = t * sc[j] + sh[j];
+        if (relu) t = fmaxf(t, 0.0f);
+      }
+      _Float16 a, b;
+      x2_split(t * s, a, b);
+      h[j] = a;
+      l[j] = b;
+    }
+    *reinterpret_cast<f16x4*>(hp) = h;
+    *reinterpret_cast<f16x4*>(lp) = l;
+  };
+  float4 rp[P_ROUNDS], rx[X_ROUNDS];
+  auto load_p = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      const int y = min(y0 + px / XTW, H - 1), x = min(x0 + px % XTW, W - 1);
+      rp[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pa.data) +
+                                               (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4);
+    }
+  };
+  auto load_x = [&](int pt) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int hp = min(idx >> 4, XHP - 1), cc = idx & 15;
+      const int y = min(max(y0 - 1 + hp / XHW, 0), H - 1), x = min(max(x0 - 1 + hp % XHW, 0), W - 1);
+      rx[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(xa.data) +
+                                               (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 4);
+    }
+  };
+  auto store_p = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < P_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      const int px = idx / (BI / 4), cc = idx % (BI / 4);
+      const bool in = y0 + px / XTW < H && x0 + px % XTW < W;
+      put(in ? rp[r] : make_float4(0, 0, 0, 0), pa.scale && in ? Ks + cc * 4 : nullptr, Ks + BI + cc * 4, pa.relu,
+          sp, &Ps[buf][0][px][cc * 4], &Ps[buf][1][px][cc * 4]);
+    }
+  };
+  auto store_x = [&](int pt, int buf) __attribute__((always_inline)) {
+    int img, y0, x0;
+    tile_origin(pt, img, y0, x0);
+#pragma unroll
+    for (int r = 0; r < X_ROUNDS; ++r) {
+      const int idx = r * 512 + tid;
+      if (idx < XHP * 16) {
+        const int hp = idx >> 4, cc = idx & 15;
+        const int y = y0 - 1 + hp / XHW, x = x0 - 1 + hp % XHW;
+        const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        put(in ? rx[r] : make_float4(0, 0, 0, 0), xa.scale && in ? Ks + 2 * BI + cc * 4 : nullptr,
+            Ks + 2 * BI + 64 + cc * 4, xa.relu, sx, &Xs[buf][0][hp][cc * 4], &Xs[buf][1][hp][cc * 4]);
+      }
+    }
+  };
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
+
+  if (pt_begin < pt_end) {
+    load_p((int)pt_begin);
+    load_x((int)pt_begin);
+    __syncthreads();  // coefficients visible
+    store_p((int)pt_begin, 0);
+    store_x((int)pt_begin, 0);
+    __syncthreads();
+  }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr8 = [&](const _Float16* p0, const _Float16* p1) __attribute__((always_inline)) {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto tile_loop = [&](auto ntc) __attribute__((always_inline)) {
+    constexpr int NTP = decltype(ntc)::value;
+    int buf = 0;
+    for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
+      const bool more = pt + 1 < (int)pt_end;
+      // the next tile goes to the free buffer in two halves (dY after k-step 1, the halo at the end),
+      // so only one half's staging registers are live at a time
+      load_p(more ? pt + 1 : pt);
+      __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
+#pragma unroll
+      for (int ks = 0; ks < XPIX / 16; ++ks) {  // two tile rows (16 pixels) per k-step
+        if (ks == 2) {
+          if (more) store_p(pt + 1, buf ^ 1);
+          load_x(more ? pt + 1 : pt);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int prow = ks * 16 + 8 * half + q4;
+        const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
+        const f16x8 ah = tr8(&Ps[buf][0][prow][pcol], &Ps[buf][0][prow + 4][pcol]);
+        const f16x8 al = tr8(&Ps[buf][1][prow][pcol], &Ps[buf][1][prow + 4][pcol]);
+        const int xcol = wj * 32 + 16 * grp_hi + 4 * p4;
+        constexpr int PF = BI == 128 ? 1 : 2;  // tap fragments read ahead (BI = 128: register-bound)
+        struct Frag {
+          f16x8 h, l;
+        };
+        auto read_tap = [&](int t) __attribute__((always_inline)) {
+          const int tap = min(tap0 + t, 8);
+          const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+          const int xrow = (2 * ks + half + dy) * XHW + dx + q4;
+          Frag f;
+          f.h = tr8(&Xs[buf][0][xrow][xcol], &Xs[buf][0][xrow + 4][xcol]);
+          f.l = tr8(&Xs[buf][1][xrow][xcol], &Xs[buf][1][xrow + 4][xcol]);
+          return f;
+        };
+        Frag bfr[NTAP];
+#pragma unroll
+        for (int t = 0; t < PF && t < NTAP; ++t) bfr[t] = read_tap(t);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + 4 * PF, 0);
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+          if (t < NTP) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bfr[t].l, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bfr[t].h, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bfr[t].h, acc[t], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+          if (t + PF < NTAP) {
+            bfr[t + PF] = read_tap(t + PF);
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+          }
+        }
+      }
+      if (more) store_x(pt + 1, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  };
+  if (TG == 1) tile_loop(std::integral_constant<int, 9>{});
+  else if (tg == 0) tile_loop(std::integral_constant<int, 5>{});
+  else tile_loop(std::integral_constant<int, 4>{});
+
+  const float ofac = uns_p * uns_x;
+  const int ctot = Q.Ctot;
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) {
+    if (t < ntap) {
+      const int tap = tap0 + t;
+      const int j = tap * ctot + c0 + wj * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        ws[split * ws_stride + (int64_t)i * ldo + j] = acc[t][r] * ofac;
+      }
+    }
+  }
+}
+
 // fp32 weight gradient (v_mfma_f32_32x32x2_f32: exact fp32 products, the parity configuration).
 // An MFMA operand is one fp32 per lane (A[i = co][k = pixel], B[k = pixel][j = ci]), read with
 // ds_read_b32 straight from the natural [pixel][channel] tiles: lanes 0-31 take pixel 2s and
@@ -1747,6 +1994,36 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(nw * 64), 0, st, p, q, co_tiles, ci_chunks, per, tiles_x, tiles_y,
                      total, ws, (int64_t)p.K * ldw, ldw);
   return check_launch("conv3x3_wgrad_wino");
+}
+
+// pixel-tile splits of the split-fp16 weight gradient: ~256 workgroups over (co tile, ci chunk, split)
+int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
+  const int bi = p.K % 128 == 0 ? 128 : 64;
+  const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
+  const int64_t total = (int64_t)q.n * cdiv(q.w, XTW) * cdiv(q.h, XTH);
+  static const int64_t target = [] {
+    const char* e = getenv("SELUNET_X2_WGRAD_WGS");
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
+  }();
+  const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
+  const int64_t per = cdiv(total, std::min(total, want));
+  if (per_out) *per_out = per;
+  return cdiv(total, per);
+}
+
+int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
+                            const float* amax_q0, const float* amax_q1, hipStream_t st) {
+  const int bi = p.K % 128 == 0 ? 128 : 64;
+  const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
+  const int tiles_x = (int)cdiv(q.w, XTW), tiles_y = (int)cdiv(q.h, XTH);
+  const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
+  int64_t per;
+  const int64_t splits = conv3x3_wgrad_x2_splits(p, q, &per);
+  const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
+  auto k = bi == 128 ? conv3x3_wgrad_x2_kernel<128> : conv3x3_wgrad_x2_kernel<64>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), 0, st, p, q, ldo, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
+                     ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1);
+  return check_launch("conv3x3_wgrad_x2");
 }
 
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype) {

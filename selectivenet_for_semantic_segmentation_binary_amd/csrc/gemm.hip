@@ -1220,6 +1220,42 @@ extern "C" int selunet_gemm_wgrad_ws_to(const selunet_gather* p, const selunet_g
   return check_launch("gemm_wgrad_ws_to");
 }
 
+// fp32 3x3 weight gradient on split-fp16 operands (conv3x3_wgrad_x2_kernel + the fixed-order split
+// reduction into the Conv2d layout)
+static int plan_wgrad_x2(const selunet_gather* p, const selunet_gather* q, WgradPlan& w) {
+  if (int rc = plan_wgrad(p, q, SELUNET_F32, w)) return rc;
+  SELUNET_REQUIRE(halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, SELUNET_F32) && w.gq.K % 9 == 0,
+                  "conv3x3_wgrad_x2: operands not eligible (P: 1 tap, K %% 64 == 0; Q: 3x3, channels %% 64 == 0, "
+                  "h >= 8, w >= 16)");
+  w.splits = conv3x3_wgrad_x2_splits(w.gp, w.gq, nullptr);
+  return 0;
+}
+
+extern "C" int64_t selunet_conv3x3_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q) {
+  WgradPlan w;
+  if (plan_wgrad_x2(p, q, w)) return -1;
+  return w.splits * (int64_t)w.ni * w.nj_pad * 4;
+}
+
+extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                        float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                                        void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad_x2(p, q, w)) return rc;
+  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  SELUNET_REQUIRE(out != nullptr && ws != nullptr && ws_bytes >= need, "conv3x3_wgrad_x2: out / workspace of %lld bytes",
+                  (long long)need);
+  SELUNET_REQUIRE(amax_p != nullptr && amax_q0 != nullptr && (q->nsrc == 1 || amax_q1 != nullptr),
+                  "conv3x3_wgrad_x2: every operand source needs its range word");
+  hipStream_t st = as_stream(stream);
+  if (int rc = conv3x3_wgrad_x2_launch(w.gp, w.gq, ws, w.nj_pad, amax_p, amax_q0, amax_q1, st)) return rc;
+  const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
+  hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
+                     (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
+  return check_launch("conv3x3_wgrad_x2");
+}
+
 // leading dimension of the packed wgrad output for a Q operand with kq columns
 extern "C" int32_t selunet_wgrad_ld(int32_t kq) {
   const int bj = (kq % 128 == 0 || kq > 512) ? 128 : 64;

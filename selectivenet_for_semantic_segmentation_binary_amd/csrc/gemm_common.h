@@ -430,6 +430,9 @@ bool conv3x3_x2_eligible(const GatherArg& g, int N);
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
+int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
+int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
+                            const float* amax_q0, const float* amax_q1, hipStream_t st);
 int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
                               hipStream_t st);
 int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int dtype, int64_t* per_out);

@@ -153,6 +153,20 @@ class Engine:
         ws = K.keep(torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=packed.device)) if wsb > 0 else None
         K.call("selunet_gemm_wgrad_ws", gp, gq, K.ptr(packed), K.ptr(ws), wsb, self.code, self.stream)
 
+    def _wgrad_x2(self, gp, gq, dyw, srcs, out):
+        """3x3 weight gradient on split-fp16 operands (selunet_conv3x3_wgrad_x2) when dY and every
+        input source carry range words and the shapes fit; False: not taken."""
+        words = [sr.amax for sr in srcs]
+        if dyw is None or any(wd is None for wd in words):
+            return False
+        wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq)
+        if wsb <= 0:
+            return False
+        ws = K.keep(torch.empty(wsb // 4, dtype=torch.float32, device=out.device))
+        K.call("selunet_conv3x3_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.ptr(out), K.ptr(dyw), K.ptr(words[0]),
+               K.ptr(words[1]) if len(words) > 1 else None, self.stream)
+        return True
+
     def _wgrad_param(self, gp, gq, layout, ni, ld, out):
         """Weight gradient straight into the parameter's gradient in the reference layout
         (layout WG_CONV3X3: [co][ci][3][3], WG_CONVT: [ci][co][2][2]); deterministic bf16 path: the
@@ -535,7 +549,8 @@ class Engine:
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
         gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
-        self._wgrad_param(gp, gq, K.WG_CONV3X3, co, ld, G[f"{name}.0.weight"])
+        if not self._wgrad_x2(gp, gq, dyw, input_srcs, G[f"{name}.0.weight"]):
+            self._wgrad_param(gp, gq, K.WG_CONV3X3, co, ld, G[f"{name}.0.weight"])
         K.marker(("grads", name))
         if not need_dgrad:
             return None
@@ -667,24 +682,28 @@ class Engine:
         u1, u2, u3 = ctx.ups["unpool1"], ctx.ups["unpool2"], ctx.ups["unpool3"]
         p1, p2, p3 = ctx.pools["pool1"], ctx.pools["pool2"], ctx.pools["pool3"]
         cb = lambda name, d, srcs, **kw: self._cbr_bwd(ctx, name, d, G, srcs, **kw)  # noqa: E731
+        uw = lambda nm: ctx.words.get("up:" + nm)  # noqa: E731  range words (split-fp16 layers)
 
         dz = cb("decoder_layer_1_1", dz, [bn["decoder_layer_1_2"].src()], prev=bn["decoder_layer_1_2"])
-        du1, dskip1 = cb("decoder_layer_1_2", dz, [K.source(u1, 64), e12.src()], dgrad_split=64)
+        du1, dskip1 = cb("decoder_layer_1_2", dz, [K.source(u1, 64, amax=uw("unpool1")), e12.src()],
+                            dgrad_split=64)
         dz = self._up_bwd(ctx, "unpool1", du1, G, bn["decoder_layer_2_1"])
         dz = cb("decoder_layer_2_1", dz, [bn["decoder_layer_2_2"].src()], prev=bn["decoder_layer_2_2"])
-        du2, dskip2 = cb("decoder_layer_2_2", dz, [K.source(u2, 128), e22.src()], dgrad_split=128)
+        du2, dskip2 = cb("decoder_layer_2_2", dz, [K.source(u2, 128, amax=uw("unpool2")), e22.src()],
+                            dgrad_split=128)
         dz = self._up_bwd(ctx, "unpool2", du2, G, bn["decoder_layer_3_1"])
         dz = cb("decoder_layer_3_1", dz, [bn["decoder_layer_3_2"].src()], prev=bn["decoder_layer_3_2"])
-        du3, dskip3 = cb("decoder_layer_3_2", dz, [K.source(u3, 256), e32.src()], dgrad_split=256)
+        du3, dskip3 = cb("decoder_layer_3_2", dz, [K.source(u3, 256, amax=uw("unpool3")), e32.src()],
+                            dgrad_split=256)
         dz = self._up_bwd(ctx, "unpool3", du3, G, bn["decoder_layer_4_1"])
         dz = cb("decoder_layer_4_1", dz, [bn["decoder_layer_4_2"].src()], prev=bn["decoder_layer_4_2"])
-        dp3 = cb("decoder_layer_4_2", dz, [K.source(p3, 256)])
+        dp3 = cb("decoder_layer_4_2", dz, [K.source(p3, 256, amax=e32.amax)])
         dz = self._pool_bwd(e32, dp3, dskip3)
         dz = cb("encoder_layer_3_2", dz, [bn["encoder_layer_3_1"].src()], prev=bn["encoder_layer_3_1"])
-        dp2 = cb("encoder_layer_3_1", dz, [K.source(p2, 128)])
+        dp2 = cb("encoder_layer_3_1", dz, [K.source(p2, 128, amax=e22.amax)])
         dz = self._pool_bwd(e22, dp2, dskip2)
         dz = cb("encoder_layer_2_2", dz, [bn["encoder_layer_2_1"].src()], prev=bn["encoder_layer_2_1"])
-        dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64)])
+        dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64, amax=e12.amax)])
         dz = self._pool_bwd(e12, dp1, dskip1)
         dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()], prev=bn["encoder_layer_1_1"])
         cb("encoder_layer_1_1", dz, [], need_dgrad=False, first_x=ctx.x)

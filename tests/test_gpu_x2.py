@@ -220,3 +220,51 @@ def test_bn_bwd_apply_amax_and_epilogue_amax():
            K.stream_ptr())
     torch.cuda.synchronize()
     assert am2.item() == up.abs().max().item()
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,xform,n,h,w", [
+    (64, 0, 64, True, 2, 16, 16),
+    (64, 64, 128, True, 2, 16, 16),     # two sources (torch.cat) of different ranges, BN+ReLU staging
+    (128, 0, 256, False, 1, 20, 36),    # ragged 8x8 tiles in both directions
+    (256, 0, 64, True, 3, 12, 18),      # ragged rows, odd tile counts, BI = 64 (two tap groups)
+    (128, 0, 128, True, 2, 9, 17),      # odd sizes
+])
+def test_x2_wgrad(cin0, cin1, cout, xform, n, h, w):
+    """Split-fp16 weight gradient (conv3x3_wgrad_x2_kernel + the fixed-order split reduction into the
+    Conv2d layout) against torch's conv2d weight gradient in fp64; gradient-sized dY (1e-9)."""
+    x0 = gen(n, cin0, h, w, seed=9)
+    s0, t0 = bn_fold(cin0, 20)
+    a0 = torch.relu(x0 * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1)) if xform else x0
+    a = a0
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    keep = [d(nhwc(x0)), d(s0), d(t0)]
+    srcs = [K.source(keep[0], cin0, keep[1] if xform else None, keep[2] if xform else None)]
+    am1 = None
+    if cin1:
+        x1 = gen(n, cin1, h, w, seed=10) * 1e-3
+        s1, t1 = bn_fold(cin1, 22)
+        a1 = torch.relu(x1 * s1.view(1, -1, 1, 1) + t1.view(1, -1, 1, 1))
+        a = torch.cat((a0, a1), 1)
+        keep += [d(nhwc(x1)), d(s1), d(t1)]
+        srcs.append(K.source(keep[3], cin1, keep[4], keep[5]))
+        am1 = word(a1.abs().max())
+    am0 = word(a0.abs().max())
+    cin = cin0 + cin1
+    wt = gen(cout, cin, 3, 3, seed=11, scale=0.05).double().requires_grad_()
+    dy = gen(n, cout, h, w, seed=12) * 1e-9
+    (ref,) = torch.autograd.grad(F.conv2d(a.double(), wt, padding=1), wt, dy.double())
+    dyd = d(nhwc(dy))
+    amp = word(dy.abs().max())
+    gp, gq = K.gather(n, h, w, 1, K.source(dyd, cout)), K.gather(n, h, w, 9, *srcs)
+    wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq)
+    assert wsb > 0
+    ws = torch.empty(wsb // 4, device=DEV)
+    outs = []
+    for _ in range(2):
+        out = torch.full((cout, cin, 3, 3), float("nan"), device=DEV)
+        K.call("selunet_conv3x3_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.ptr(out), K.ptr(amp), K.ptr(am0), K.ptr(am1),
+               K.stream_ptr())
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert rel(outs[0].cpu(), ref) < TOL
+    assert torch.equal(outs[0], outs[1])  # fixed-order reduction: bit-reproducible
