@@ -7,9 +7,10 @@ fp32 in, `(N,H,W)` logits out, or the `(out, select, aux)` triple when selective
 (model.py:98-103). The modules inside `CBR_2D` are parameter containers only; the forward
 runs entirely in libselunet.so through one autograd.Function (`_UNetBFunction`).
 
-Extra keyword (not in the reference): `compute_dtype` — torch.float32 (default; exact fp32
-MFMA, the parity configuration) or torch.bfloat16 (bf16 operands, fp32 accumulation,
-statistics, losses and master weights).
+Extra keyword (not in the reference): `compute_dtype` — torch.float32 (default, the parity
+configuration: fp32 tensors; in training the 3x3 convolutions run on split-fp16 operands with an
+error at or below the exact fp32 MFMA's, SELUNET_X2=0 selects exact fp32 MFMA products) or
+torch.bfloat16 (bf16 operands, fp32 accumulation, statistics, losses and master weights).
 """
 from __future__ import annotations
 

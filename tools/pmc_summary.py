@@ -26,7 +26,12 @@ def _pat(base, *targs):
     return rf"{base}I{m}|{re.escape(base + '<' + d)}[,>]" if targs else base
 
 
-NAME_MAP = []
+NAME_MAP = [
+    (_pat("conv3x3_halo_persist_kernel", "f32", 128, "true"), "conv3x3_x2<f32,128>"),
+    (_pat("conv3x3_halo_persist_kernel", "f32", 64, "true"), "conv3x3_x2<f32,64>"),
+    (_pat("conv3x3_wgrad_x2_kernel", 128), "conv3x3_wgrad_x2<128>"),
+    (_pat("conv3x3_wgrad_x2_kernel", 64), "conv3x3_wgrad_x2<64>"),
+]
 for _t in ("bf16", "f32"):
     NAME_MAP += [
         (_pat("conv3x3_halo_persist_kernel", _t, 128), f"conv3x3_halo_persist<{_t},128>"),
@@ -76,15 +81,20 @@ def load(path):
     return agg, calls, dur
 
 
-def report(path, top=12):
-    agg, calls, dur = load(path)
+def report(paths, top=12):
+    agg, calls, dur = load(paths[0])
+    for p in paths[1:]:  # counter passes of the same program, kernels matched by name
+        a2, _, _ = load(p)
+        for k, v in a2.items():
+            for ctr, x in v.items():
+                agg[k].setdefault(ctr, x)
     keys = sorted(agg, key=lambda k: -sum(dur[k].values()))
     for k in keys[:top]:
         c = agg[k]
         n = len(calls[k])
         t = sum(dur[k].values())
         line = f"{t / 1e6:8.2f} ms {n:4d} calls {short(k)[:40]:40s}"
-        if "SQ_WAVE_CYCLES" in c:
+        if "SQ_WAVE_CYCLES" in c and "SQ_WAIT_ANY" in c:
             wc = c["SQ_WAVE_CYCLES"]
             line += (f" wait {c['SQ_WAIT_ANY'] / wc:5.2f} waitinst {c['SQ_WAIT_INST_ANY'] / wc:5.2f} "
                      f"active {c['SQ_ACTIVE_INST_ANY'] / wc:5.2f} ldsconf/wc {c['SQ_LDS_BANK_CONFLICT'] / wc:6.3f}")
@@ -131,4 +141,5 @@ if __name__ == "__main__":
     if sys.argv[1] == "--traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4])
     else:
-        report(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 12)
+        report([a for a in sys.argv[1:] if a.endswith(".csv")],
+               int(sys.argv[-1]) if not sys.argv[-1].endswith(".csv") else 12)
