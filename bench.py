@@ -83,7 +83,8 @@ class KernelTimer:
     dispatches to, with its algorithmic FLOPs (2*M*N*K of the true, unpadded GEMM) and algorithmic
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
-    MFMA = ("selunet_gemm_gather", "selunet_conv3x3_wino", "selunet_conv3x3_x2", "selunet_conv3x3_wgrad_x2",
+    MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
+            "selunet_conv3x3_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
@@ -115,6 +116,13 @@ class KernelTimer:
             flops = 2.0 * m * n_cols * self._k(g)
             nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
             return kname, "mfma", flops, nbytes, f"gather {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}"
+        if name == "selunet_gemm_gather_x2":  # (g, w, n_cols, k_pad, ep, amax0, amax1, stream)
+            g, n_cols, mode = args[0], _i(args[2]), args[4].mode
+            m = g.n * g.h * g.w
+            flops = 3 * 2.0 * m * n_cols * self._k(g)  # executed fp16 MFMA work
+            nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
+            return ("gemm_gather_x2<f32>", "mfma_f16", flops, nbytes,
+                    f"gather x2 {g.h}x{g.w} taps={g.taps} K={self._k(g)} N={n_cols} mode={mode}")
         if name == "selunet_conv3x3_wino":  # (g, u, n_cols, ep, stream): fp32 Winograd F(2,3)
             g, n_cols, ep = args[0], _i(args[2]), args[3]
             kname = K.query("selunet_conv3x3_wino_kernel_name", n_cols, ep.mode, ep.split).decode()

@@ -152,6 +152,11 @@ const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32
  * SELUNET_PACK_CONV3X3_X2 pack ([n_cols][9*C] + n_cols row unscale factors). Same gathers,
  * epilogues and statistics slab rows as selunet_gemm_gather; selunet_conv3x3_x2_ok tells whether a
  * layer can take it (h, w >= 16, C and c_src0 multiples of 32, C > 32, n_cols a multiple of 64). */
+/* selunet_gemm_gather on split-fp16 operands (ConvTranspose2d forward / data gradient in fp32 training,
+ * model.py:44,51,57): w a split-fp16 pack (SELUNET_PACK_CONVT_X2 rows, k_pad == K, K a multiple of 32),
+ * amax0 / amax1 the sources' range words; any gather taps and epilogue of selunet_gemm_gather. */
+int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, int32_t n_cols, int32_t k_pad,
+                           const selunet_epilogue* ep, const float* amax0, const float* amax1, void* stream);
 int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
 /* fp32 3x3 weight gradient (autograd of model.py:11's weight) on split-fp16 operands, the same
  * arithmetic as selunet_conv3x3_x2: p = dY (1 tap, [M][co]), q = the layer input (3x3 gather, BN+ReLU
@@ -226,7 +231,15 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * (max|w_row| * 2^e_row < 2^14) and every 32-k group (one tap, 32 channels) stored as 32 fp16 high
  * parts h = fp16(v) then 32 low parts l = fp16(v - h); the row unscale factors 2^-e_row follow the
  * matrix: fwd + co*9*ci (co floats), dgrad + ci*9*co (ci floats). ci, co multiples of 32. */
-enum { SELUNET_PACK_CONV3X3 = 0, SELUNET_PACK_CONVT = 1, SELUNET_PACK_CONV3X3_WINO = 2, SELUNET_PACK_CONV3X3_X2 = 3 };
+/* SELUNET_PACK_CONVT_X2 (fp32): the same split-fp16 format for a ConvTranspose2d weight [ci][co][2][2]:
+ * fwd = [4*co][ci] (row (a*2+b)*co + o, k_pad = ci) + 4*co unscale factors, dgrad = [ci][4*co] + ci. */
+enum {
+  SELUNET_PACK_CONV3X3 = 0,
+  SELUNET_PACK_CONVT = 1,
+  SELUNET_PACK_CONV3X3_WINO = 2,
+  SELUNET_PACK_CONV3X3_X2 = 3,
+  SELUNET_PACK_CONVT_X2 = 4
+};
 typedef struct selunet_pack_desc {
   const float* w;
   void* fwd;

@@ -49,7 +49,7 @@ class PackDesc(ctypes.Structure):
                 ("ci", c_int32), ("k_pad", c_int32), ("offset", c_int64)]
 
 
-PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2 = 24, 0, 1, 2, 3
+PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2, PACK_CONVT_X2 = 24, 0, 1, 2, 3, 4
 WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
 
 
@@ -88,6 +88,8 @@ SIGNATURES = {
     "selunet_conv3x3_wino": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P]),
     "selunet_conv3x3_wino_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
     "selunet_conv3x3_x2_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "selunet_gemm_gather_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, c_int32, ctypes.POINTER(Epilogue), P, P,
+                                         P]),
     "selunet_conv3x3_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
     "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
     "selunet_act_bound": (c_int32, [P, P, c_int32, c_int64, P, P]),

@@ -549,6 +549,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   using Acc = std::conditional_t<X2 && BN == 128, float, typename StatAcc<T>::type>;
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float amx = 0.0f;  // running max |stored value| (epilogue range word)
   const TileStats ts = tile_stats(ep, prow, n0, N);
   float* tile = reinterpret_cast<float*>(smem);  // epilogue: [256][BN + 4] over the whole LDS
   uint4 ra[A_ROUNDS];
@@ -649,7 +650,8 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       return reinterpret_cast<T*>(ep.out0) + m * N + col;
     };
     auto bias_col = [&](int cl) { return n0 + cl; };
-    if (!(SELUNET_ABL & 32)) lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+    if (!(SELUNET_ABL & 32))
+      lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
     if (i + 1 < ntl) {
       __syncthreads();  // the tile has been read: LDS back to halo / weights
       int nimg, ny0, nx0;
@@ -662,7 +664,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       __syncthreads();
     }
   }
-  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3);
+  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
 }
 
 // =========================================================================== fp32 Winograd F(2,3)
@@ -877,6 +879,7 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
   using Acc = std::conditional_t<BN == 128, float, typename StatAcc<T>::type>;
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float amx = 0.0f;  // running max |stored value| (epilogue range word)
   const TileStats ts = tile_stats(ep, prow, n0, N);
   float* tile = reinterpret_cast<float*>(smem);
   uint4 ra[A_ROUNDS];
@@ -976,7 +979,7 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
       return reinterpret_cast<T*>(ep.out0) + m * N + col;
     };
     auto bias_col = [&](int cl) { return n0 + cl; };
-    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
     if (i + 1 < ntl) {
       __syncthreads();
       int nimg, ny0, nx0;
@@ -989,7 +992,7 @@ conv3x3_wino_persist_kernel(GatherArg g, const float* __restrict__ B, int N, int
       __syncthreads();
     }
   }
-  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3);
+  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
 }
 
 // =========================================================================== weight gradient

@@ -40,9 +40,17 @@ namespace selunet {
 // latency + one exposed epilogue per tile). Statistics accumulate in registers over the tiles and
 // are written once per workgroup (slab row prow). P = number of row tiles gives the one-tile-per-
 // workgroup launch.
-template <typename T, int BN, bool SMALL>
+//
+// X2 (fp32, vector gathers only): the split-fp16 form (selunet_gemm_gather_x2; ConvTranspose2d forward
+// and data gradient in fp32 training): every staged A value is scaled by 2^e (range words amax0/amax1)
+// and written as fp16 high / low parts into the 128-B K slice (bytes 0-63 high, 64-127 low), B is a
+// split-fp16 pack of the same layout (row unscale factors in wcs), three v_mfma_f32_32x32x16_f16 per
+// 16-k step, accumulators unscaled before the epilogue — as conv3x3_halo_persist_kernel<.., X2>.
+template <typename T, int BN, bool SMALL, bool X2>
 __global__ void __launch_bounds__(256, 2)
-gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int P) {
+gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int P,
+                   const float* __restrict__ wcs, const float* __restrict__ amax0, const float* __restrict__ amax1) {
+  static_assert(!X2 || (std::is_same<T, float>::value && !SMALL), "split-fp16 form: fp32 vector gathers");
   constexpr int E = 16 / sizeof(T);          // elements per 16-B vector
   constexpr int BKE = 128 / sizeof(T);       // K elements per stage
   constexpr int WN = BN / 2;                 // wave tile columns
@@ -72,6 +80,35 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 
   const int cc = tid & 7;       // 16-B chunk within the 128-B K slice
   const int rr = tid >> 3;      // base row (0..31)
+  float xs = 1.0f;              // X2: operand scale 2^e
+  float cfac[NT] = {};          // X2: accumulator unscale per 32-column subtile (this lane's column)
+  if constexpr (X2) {
+    float am = amax0 ? amax0[0] : 0.0f;
+    if (g.nsrc > 1 && amax1) am = fmaxf(am, amax1[0]);
+    float inv;
+    xs = x2_scale(am, &inv);
+#pragma unroll
+    for (int b = 0; b < NT; ++b) cfac[b] = wcs[n0 + wn * WN + b * 32 + l32] * inv;
+  }
+  // A row value quad -> LDS (X2: scaled and split into the high / low halves of the K slice)
+  auto put_a = [&](unsigned char* a_dst, int row, uint4 v) __attribute__((always_inline)) {
+    if constexpr (X2) {
+      float f[4];
+      __builtin_memcpy(f, &v, 16);
+      f16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        _Float16 x, y;
+        x2_split(f[e] * xs, x, y);
+        h[e] = x;
+        l[e] = y;
+      }
+      *reinterpret_cast<f16x4*>(a_dst + row * ROWB + cc * 8) = h;
+      *reinterpret_cast<f16x4*>(a_dst + row * ROWB + 64 + cc * 8) = l;
+    } else {
+      *reinterpret_cast<uint4*>(a_dst + row * ROWB + cc * 16) = v;
+    }
+  };
 
   // One staged K slice, held in registers between its loads and its LDS write. Loads are issued
   // unconditionally (rows / pixels clamped to valid addresses, zeroed when written to LDS) so the
@@ -163,13 +200,11 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
         }
         uint4 o;
         __builtin_memcpy(&o, v, 16);
-        *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) = o;
+        put_a(a_dst, rr + 32 * i, o);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AR; ++i)
-        *reinterpret_cast<uint4*>(a_dst + (rr + 32 * i) * ROWB + cc * 16) =
-            ((st.ok >> i) & 1u) ? st.a[i] : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < AR; ++i) put_a(a_dst, rr + 32 * i, ((st.ok >> i) & 1u) ? st.a[i] : make_uint4(0, 0, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
@@ -179,6 +214,33 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   auto mma_stage = [&](f32x16 (&acc)[MT][NT], int buf) __attribute__((always_inline)) {
     const unsigned char* a_src = As + buf * BM * ROWB;
     const unsigned char* b_src = Bs + buf * BN * ROWB;
+    if constexpr (X2) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        f16x8 ah[MT], al[MT], bh[NT], bl[NT];
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          const unsigned char* p = a_src + (wm * 64 + a * 32 + l32) * ROWB + half * 16;
+          ah[a] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          al[a] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const unsigned char* p = b_src + (wn * WN + b * 32 + l32) * ROWB + half * 16;
+          bh[b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          bl[b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int boff = q * 32 + half * 16;
@@ -208,8 +270,15 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   using Acc = typename StatAcc<T>::type;
   static_assert(stats_flush_bytes<BN, 256, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto epilogue = [&](const f32x16 (&acc)[MT][NT], int64_t m_tile) __attribute__((always_inline)) {
+  float amx = 0.0f;  // running max |stored value| (epilogue range word)
+  auto epilogue = [&](f32x16 (&acc)[MT][NT], int64_t m_tile) __attribute__((always_inline)) {
     const int64_t m0 = m_tile * BM;
+    if constexpr (X2) {
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] *= cfac[b];
+    }
     acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
     // SCATTER2X: each tile row's output base (pixel (img, 2y, 2x) of the 2x-upsampled grid) decoded
     // once into LDS past the tile, instead of three integer divisions per stored 16-B chunk
@@ -240,7 +309,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     };
     auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
     if (!(SELUNET_GABL & 1))
-      lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3);
+      lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
   };
 
   f32x16 acc[MT][NT];
@@ -324,7 +393,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     kc = nkc;
   }
 #endif
-  tile_stats_flush<BN, 256>(tile, tid, ts, s1, s2, s3);
+  tile_stats_flush<BN, 256>(tile, tid, ts, s1, s2, s3, amx);
 }
 
 // =========================================================================== gemm_wgrad
@@ -773,8 +842,8 @@ template <typename T, int BN, bool SMALL>
 static void launch_gather_impl(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, hipStream_t st) {
   const int n_tiles = N / BN;
   const int64_t P = gather_rows(g, N);
-  hipLaunchKernelGGL((gemm_gather_kernel<T, BN, SMALL>), dim3((unsigned)(P * n_tiles)), dim3(256), 0, st, g,
-                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, (int)P);
+  hipLaunchKernelGGL((gemm_gather_kernel<T, BN, SMALL, false>), dim3((unsigned)(P * n_tiles)), dim3(256), 0, st, g,
+                     reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, (int)P, nullptr, nullptr, nullptr);
 }
 
 template <typename T, int BI, int BJ>
@@ -932,6 +1001,29 @@ extern "C" int selunet_conv3x3_wino(const selunet_gather* a, const float* u, int
                   "conv3x3_wino: operand not eligible (%dx%d, C=%d, n_cols=%d; see selunet_conv3x3_wino_ok)", g.h, g.w,
                   g.Ctot, n_cols);
   return conv3x3_wino_launch(g, u, n_cols, e, as_stream(stream));
+}
+
+extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, int32_t n_cols, int32_t k_pad,
+                                      const selunet_epilogue* ep, const float* amax0, const float* amax1,
+                                      void* stream) {
+  GatherArg g;
+  EpiArg e;
+  if (int rc = check_gather_call(a, w, n_cols, k_pad, ep, SELUNET_F32, g, e)) return rc;
+  SELUNET_REQUIRE(!g.small && k_pad == g.K && g.K % 32 == 0,
+                  "gemm_gather_x2: vector gathers with K (%d) a multiple of 32 and k_pad == K", g.K);
+  SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
+                  "gemm_gather_x2: every source needs its range word (amax0, amax1)");
+  hipStream_t st = as_stream(stream);
+  const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
+  const int64_t P = gather_rows(g, n_cols);
+  const float* wcs = w + (int64_t)n_cols * k_pad;
+  if (bn128)
+    hipLaunchKernelGGL((gemm_gather_kernel<float, 128, false, true>), dim3((unsigned)(P * (n_cols / 128))), dim3(256),
+                       0, st, g, w, n_cols, k_pad, e, n_cols / 128, (int)P, wcs, amax0, amax1);
+  else
+    hipLaunchKernelGGL((gemm_gather_kernel<float, 64, false, true>), dim3((unsigned)(P * (n_cols / 64))), dim3(256), 0,
+                       st, g, w, n_cols, k_pad, e, n_cols / 64, (int)P, wcs, amax0, amax1);
+  return check_launch("gemm_gather_x2");
 }
 
 extern "C" int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols) {

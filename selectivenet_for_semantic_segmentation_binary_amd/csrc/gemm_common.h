@@ -261,7 +261,7 @@ template <> struct StatAcc<float> { using type = double; };
 template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol, typename Acc>
 __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& dst, const float* bias,
                                                    BiasCol&& bias_col, const TileStats& ts, Acc (&s1)[8],
-                                                   Acc (&s2)[8], Acc (&s3)[8]) {
+                                                   Acc (&s2)[8], Acc (&s3)[8], float& am) {
   constexpr int CC = TC / 8;            // 8-column chunks per row
   constexpr int RS = NTHREADS / CC;     // rows per pass
   // an opaque copy of tid: in a persistent kernel the column coefficients below are invariant over
@@ -291,7 +291,6 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
   float* t1 = WIDE ? tw1 : reinterpret_cast<float*>(s1);
   float* t2 = WIDE ? tw2 : reinterpret_cast<float*>(s2);
   float* t3 = WIDE ? tw3 : reinterpret_cast<float*>(s3);
-  float am = 0.0f;
   for (int row = r0; row < TR; row += RS) {
     T* p = dst(row, col);
     if (p == nullptr) continue;
@@ -348,7 +347,6 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       }
     }
   }
-  if (ts.amax) atomic_amax(ts.amax, am);
   if constexpr (WIDE) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -368,7 +366,10 @@ constexpr int stats_flush_bytes() { return (NTHREADS / (TC / 8)) * TC * 3 * (int
 // row (fp32).
 template <int TC, int NTHREADS, typename Acc>
 __device__ __forceinline__ void tile_stats_flush(float* red_f, int tid, const TileStats& ts, const Acc (&s1)[8],
-                                                 const Acc (&s2)[8], const Acc (&s3)[8]) {
+                                                 const Acc (&s2)[8], const Acc (&s3)[8], float am) {
+  // the running max |stored value| of this thread's tiles: one atomic per wave per workgroup (an atomic
+  // per tile put 0.5M same-address atomics into a full-resolution launch)
+  if (ts.amax) atomic_amax(ts.amax, am);
   constexpr int CC = TC / 8;
   constexpr int RS = NTHREADS / CC;
   Acc* red = reinterpret_cast<Acc*>(red_f);
@@ -401,8 +402,9 @@ template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasC
 __device__ __forceinline__ void lds_tile_store(float* tile, int tid, Dst&& dst, const float* bias, BiasCol&& bias_col,
                                                const TileStats& ts) {
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  lds_tile_store_acc<T, TR, TC, NTHREADS>(tile, tid, dst, bias, bias_col, ts, s1, s2, s3);
-  tile_stats_flush<TC, NTHREADS>(tile, tid, ts, s1, s2, s3);
+  float am = 0.0f;
+  lds_tile_store_acc<T, TR, TC, NTHREADS>(tile, tid, dst, bias, bias_col, ts, s1, s2, s3, am);
+  tile_stats_flush<TC, NTHREADS>(tile, tid, ts, s1, s2, s3, am);
 }
 
 // host: validate a C-ABI gather descriptor and convert it (gemm.hip)

@@ -165,13 +165,19 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
   while (t + 1 < l.n && b >= l.d[t + 1].offset) ++t;
   const selunet_pack_desc& d = l.d[t];
   const int co = d.co, ci = d.ci;
+  const bool ct = d.kind == SELUNET_PACK_CONVT_X2;  // ConvTranspose2d [ci][co][2][2]
+  const int fwd_rows = ct ? 4 * co : co;
   const int r = (int)(b - d.offset);
-  const bool fw = r < co;
-  const int row = fw ? r : r - co;
-  const int len = fw ? 9 * ci : 9 * co;
-  const int rk = fw ? ci : co;  // k = tap * rk + channel
+  const bool fw = r < fwd_rows;
+  const int row = fw ? r : r - fwd_rows;
+  const int len = ct ? (fw ? ci : 4 * co) : (fw ? 9 * ci : 9 * co);
+  const int rk = fw ? ci : co;  // conv3x3: k = tap * rk + channel
   const float* w = d.w;
   auto val = [&](int k) -> float {
+    if (ct) {  // fwd row (ab, o) = ab * co + o, k = c; dgrad row c, k = ab * co + o
+      const int ab = fw ? row / co : k / co, o = fw ? row - ab * co : k - (k / co) * co, c = fw ? k : row;
+      return w[((int64_t)c * co + o) * 4 + ab];
+    }
     const int tap = k / rk, c = k - tap * rk;
     return fw ? w[((int64_t)row * ci + c) * 9 + tap] : w[((int64_t)c * ci + row) * 9 + (8 - tap)];
   };
@@ -185,7 +191,7 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
     __syncthreads();
   }
   float* base = reinterpret_cast<float*>(fw ? d.fwd : d.dgrad);
-  const int rows = fw ? co : ci;
+  const int rows = fw ? fwd_rows : ci;
   float unscale;
   const float sc = x2_scale(red[0], &unscale);
   _Float16* out = reinterpret_cast<_Float16*>(base + (int64_t)row * len);
@@ -198,6 +204,10 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
     out[grp * 64 + 32 + j] = lo;
   }
   if (threadIdx.x == 0) base[(int64_t)rows * len + row] = unscale;
+}
+
+__global__ void fill_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
 static unsigned grid_for(int64_t n, int64_t cap = 4096) {
@@ -1254,13 +1264,16 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
     selunet_pack_desc& d = l.d[t];
     SELUNET_REQUIRE(d.w && (d.fwd || d.dgrad) && d.co > 0 && d.ci > 0, "pack_weights: bad entry %d", t);
     d.offset = off;
-    if (d.kind == SELUNET_PACK_CONV3X3_X2) {
-      SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == 9 * d.ci && d.ci % 32 == 0 && d.co % 32 == 0,
-                      "pack_weights: split-fp16 entry %d needs fp32, fwd, k_pad = 9*ci and ci, co multiples of 32", t);
+    if (d.kind == SELUNET_PACK_CONV3X3_X2 || d.kind == SELUNET_PACK_CONVT_X2) {
+      const bool ct = d.kind == SELUNET_PACK_CONVT_X2;
+      SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == (ct ? d.ci : 9 * d.ci) && d.ci % 32 == 0 &&
+                          d.co % 32 == 0,
+                      "pack_weights: split-fp16 entry %d needs fp32, fwd, k_pad = %s and ci, co multiples of 32", t,
+                      ct ? "ci" : "9*ci");
       lx.d[lx.n] = d;
       lx.d[lx.n].offset = xrows;
       ++lx.n;
-      xrows += d.co + (d.dgrad ? d.ci : 0);
+      xrows += (ct ? 4 * d.co : d.co) + (d.dgrad ? d.ci : 0);
     } else if (d.kind == SELUNET_PACK_CONV3X3) {
       SELUNET_REQUIRE(d.fwd && d.k_pad >= 9 * d.ci, "pack_weights: bad conv3x3 entry %d", t);
       off += (int64_t)d.co * d.k_pad + (d.dgrad ? (int64_t)d.ci * 9 * d.co : 0);
@@ -1297,6 +1310,15 @@ int selunet_unpack_convT_grad(const float* packed, int32_t ci, int32_t co, float
 
 int selunet_memset(void* dst, int32_t value, int64_t bytes, void* stream) {
   SELUNET_REQUIRE(dst && bytes >= 0, "memset: bad arguments");
+  if (bytes && reinterpret_cast<uintptr_t>(dst) % 4 == 0 && bytes % 4 == 0) {
+    // a kernel, not hipMemsetAsync: inside captured HIP graphs small memset nodes were seen to leave the
+    // target unwritten on the second launch of the graph (tests/test_gpu_graphs.py)
+    const uint32_t v = (uint32_t)(value & 0xff) * 0x01010101u;
+    const int64_t n = bytes / 4;
+    hipLaunchKernelGGL(fill_u32_kernel, dim3(grid_for(n, 4096)), dim3(TPB), 0, as_stream(stream),
+                       reinterpret_cast<uint32_t*>(dst), n, v);
+    return check_launch("memset");
+  }
   if (bytes && hipMemsetAsync(dst, value, (size_t)bytes, as_stream(stream)) != hipSuccess)
     return fail(SELUNET_ELAUNCH, "hipMemsetAsync failed");
   return 0;

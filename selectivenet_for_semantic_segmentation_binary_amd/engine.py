@@ -246,13 +246,19 @@ class Engine:
             pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), kind, co, ci, kpad, 0)
             pl.n += 1
             packs[name] = WPack(fwd, dg, kpad, co, mode)
+        x2 = any(wp.mode == "x2" for wp in packs.values())
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
-            fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
-            dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
-            pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
+            if x2:  # ConvTranspose2d forward / data gradient on split-fp16 operands (selunet_gemm_gather_x2)
+                fwd = K.keep(torch.empty(4 * co * ci + 4 * co, dtype=torch.float32, device=dev))
+                dg = K.keep(torch.empty(ci * 4 * co + ci, dtype=torch.float32, device=dev)) if need_dgrad else None
+                pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT_X2, co, ci, ci, 0)
+            else:
+                fwd = K.keep(torch.empty(4 * co, ci, dtype=self.dt, device=dev))
+                dg = K.keep(torch.empty(ci, 4 * co, dtype=self.dt, device=dev)) if need_dgrad else None
+                pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
             pl.n += 1
-            packs[name] = WPack(fwd, dg, ci, co)
+            packs[name] = WPack(fwd, dg, ci, co, "x2" if x2 else "direct")
         K.call("selunet_pack_weights", pl, self.code, self.stream)
         return packs
 
@@ -351,7 +357,10 @@ class Engine:
         ep = K.Epilogue(K.ptr(out), None, K.ptr(P[f"{name}.bias"]), None, K.EP_SCATTER2X, 0)
         if ctx.x2:  # range word of the up-sampled tensor (exact max, the epilogue's atomic)
             ep.amax = K.ptr(self._word(ctx, "up:" + name))
-        K.call("selunet_gemm_gather", g, K.ptr(fwd), 4 * co, ci, ep, self.code, self.stream)
+        if wp.mode == "x2":
+            K.call("selunet_gemm_gather_x2", g, K.ptr(fwd), 4 * co, ci, ep, K.ptr(st.amax), None, self.stream)
+        else:
+            K.call("selunet_gemm_gather", g, K.ptr(fwd), 4 * co, ci, ep, self.code, self.stream)
         ctx.ups[name] = out
         return out
 
@@ -427,7 +436,7 @@ class Engine:
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W), training=training)
         ctx.x2 = any(wp.mode == "x2" for wp in ctx.wpack.values())
         if ctx.x2:  # the operand range words of this step, zeroed for their atomic-max producers
-            keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy")]
+            keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy", "du")]
             keys += ["up:" + nm for nm, _, _ in LY.UNPOOLS]
             buf = K.keep(torch.empty(len(keys), dtype=torch.float32, device=x.device))
             K.call("selunet_memset", K.ptr(buf), 0, buf.numel() * 4, self.stream)
@@ -572,6 +581,8 @@ class Engine:
         d1 = K.keep(torch.empty(M, ci - c0, dtype=self.dt, device=dev))
         colsum = K.keep(torch.empty(rows, c0, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, c0, K.ptr(colsum))
+        if ctx.x2:  # a bound on d(up) (both halves' max): the split-fp16 ConvTranspose2d data gradient reads it
+            ep.amax = K.ptr(self._word(ctx, "du:" + name))
         self._conv3x3(ga, wd, ci, 9 * co, ep, wp.mode, (dsrc,))
         return DGrad(d0, colsum, rows), d1
 
@@ -594,7 +605,11 @@ class Engine:
         slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = bnb_for(prev, slab)
-        K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
+        if wp.mode == "x2":
+            duw = self._word(ctx, "du:decoder_layer_" + name[-1] + "_2")  # unpool k feeds decoder_layer_k_2
+            K.call("selunet_gemm_gather_x2", ga, K.ptr(wd), ci, 4 * co, ep, K.ptr(duw), None, self.stream)
+        else:
+            K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
         return DGrad(dz, slab, rows)
 
     def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
