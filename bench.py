@@ -84,7 +84,7 @@ class KernelTimer:
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
     MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
-            "selunet_conv3x3_wgrad_x2",
+            "selunet_conv3x3_wgrad_x2", "selunet_gemm_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
@@ -148,6 +148,12 @@ class KernelTimer:
             flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             return kname, "mfma_f16", flops, nbytes, f"wgrad x2 {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
+        if name == "selunet_gemm_wgrad_x2":  # (gp, gq, ws, wsb, layout, out, amax_p0, p1, q0, q1, stream)
+            gp, gq = args[0], args[1]
+            flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work
+            nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
+            return ("gemm_wgrad_x2<f32>+reduce", "mfma_f16", flops, nbytes,
+                    f"wgrad gx2 {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}")
         if name in ("selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to"):
             gp, gq = args[0], args[1]
             dt = _i(args[{"selunet_gemm_wgrad": 3, "selunet_gemm_wgrad_ws": 5, "selunet_gemm_wgrad_ws_to": 7}[name]])

@@ -157,6 +157,14 @@ const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32
  * amax0 / amax1 the sources' range words; any gather taps and epilogue of selunet_gemm_gather. */
 int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, int32_t n_cols, int32_t k_pad,
                            const selunet_epilogue* ep, const float* amax0, const float* amax1, void* stream);
+/* selunet_gemm_wgrad_ws_to on split-fp16 operands (the ConvTranspose2d weight gradient in fp32 training,
+ * layout SELUNET WG_CONVT = 2, or a Conv2d one, layout 1): vector gathers, K_p and K_q multiples of 64;
+ * amax_p0/p1, amax_q0/q1 the sources' range words (p1 / q1 only for two-source gathers). Partials in
+ * ws (>= selunet_gemm_wgrad_x2_ws_bytes), summed in a fixed order into out. */
+int64_t selunet_gemm_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q);
+int selunet_gemm_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes, int32_t layout,
+                          float* out, const float* amax_p0, const float* amax_p1, const float* amax_q0,
+                          const float* amax_q1, void* stream);
 int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
 /* fp32 3x3 weight gradient (autograd of model.py:11's weight) on split-fp16 operands, the same
  * arithmetic as selunet_conv3x3_x2: p = dY (1 tap, [M][co]), q = the layer input (3x3 gather, BN+ReLU

@@ -533,6 +533,181 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
     }
 }
 
+// =========================================================================== gemm_wgrad (split fp16)
+// fp32 weight gradient on split-fp16 operands (selunet_gemm_wgrad_x2: the ConvTranspose2d weight
+// gradient in fp32 training): the bf16 kernel's structure (natural [pixel][column] LDS tiles,
+// ds_read_b64_tr_b16 operand reads) with each fp32 operand column scaled by its source's 2^e and
+// stored as two fp16 planes (high, low); three v_mfma_f32_32x32x16_f16 per 16-pixel step (hl, lh,
+// hh); each output (i, j) is unscaled by its two columns' 2^-e before the split partial is written.
+template <int BI, int BJ>
+__global__ void __launch_bounds__(256, 2)
+gemm_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int64_t mchunk, int tiles_j, int tiles, float* __restrict__ ws,
+                     int64_t ws_stride, const float* __restrict__ amax_p0, const float* __restrict__ amax_p1,
+                     const float* __restrict__ amax_q0, const float* __restrict__ amax_q1) {
+  constexpr int KM = 32;                           // pixels per stage
+  constexpr int PADE = 32;                         // 64 B row pad (bank spread for tr reads)
+  constexpr int LDI = BI + PADE, LDJ = BJ + PADE;  // row strides in halves
+  constexpr int WI = BI / 2, WJ = BJ / 2;
+  constexpr int MT = WI / 32, NT = WJ / 32;
+  constexpr int CPI = BI / 4, CPJ = BJ / 4;        // 16-B fp32 chunks per row
+  constexpr int RPI = 256 / CPI, RPJ = 256 / CPJ;
+  constexpr int PI = KM / RPI, PJ = KM / RPJ;
+  static_assert(PI >= 1 && PJ >= 1, "stage rows must cover the threads");
+
+  __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][KM][LDI];
+  __shared__ __attribute__((aligned(16))) _Float16 Qs[2][2][KM][LDJ];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lb % tiles;
+  const int64_t split = lb / tiles;
+  const int i0 = (tile / tiles_j) * BI;
+  const int j0 = (tile % tiles_j) * BJ;
+  const int64_t mb = split * mchunk;
+  const int64_t me = min(P.M, mb + mchunk);
+
+  const int pc = tid % CPI, pr = tid / CPI;
+  const int qc = tid % CPJ, qr = tid / CPJ;
+  const int pk = i0 + pc * 4, qk = j0 + qc * 4;
+  int ptap = pk / P.Ctot, pch = pk - ptap * P.Ctot, ps = 0;
+  if (P.nsrc > 1 && pch >= P.src[0].C) { pch -= P.src[0].C; ps = 1; }
+  int qtap = qk / Q.Ctot, qch = qk - qtap * Q.Ctot, qs = 0;
+  if (Q.nsrc > 1 && qch >= Q.src[0].C) { qch -= Q.src[0].C; qs = 1; }
+  const bool pin = pk < P.K, qin = qk < Q.K;
+  const SrcArg psa = pick_src(P, ps), qsa = pick_src(Q, qs);
+  const float sp = x2_scale((ps ? amax_p1 : amax_p0)[0], nullptr);
+  const float sq = x2_scale((qs ? amax_q1 : amax_q0)[0], nullptr);
+  float psc[4], psh[4], qsc[4], qsh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    psc[e] = psa.scale && pin ? psa.scale[pch + e] : 1.0f;
+    psh[e] = psa.scale && pin ? psa.shift[pch + e] : 0.0f;
+    qsc[e] = qsa.scale && qin ? qsa.scale[qch + e] : 1.0f;
+    qsh[e] = qsa.scale && qin ? qsa.shift[qch + e] : 0.0f;
+  }
+  float4 rp[PI], rq[PJ];
+  unsigned pok = 0, qok = 0;  // bit i: staged row i is a real (non-padding) pixel
+  auto raw_row = [&](const GatherArg& g, const SrcArg& sa, int64_t m, int tap, int c, bool in, unsigned& ok,
+                     int bit) __attribute__((always_inline)) {
+    int64_t pix = (in && m < me) ? src_index(g, m, tap) : -1;
+    ok |= (pix >= 0 ? 1u : 0u) << bit;
+    pix = pix >= 0 ? pix : 0;
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(sa.data) + pix * sa.C + c);
+  };
+  auto put = [&](float4 raw, bool ok, const SrcArg& sa, const float* sc, const float* sh, float s, _Float16* hp,
+                 _Float16* lp) __attribute__((always_inline)) {
+    float f[4] = {raw.x, raw.y, raw.z, raw.w};
+    f16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = f[e];
+      if (sa.scale) {
+        t = t * sc[e] + sh[e];
+        if (sa.relu) t = fmaxf(t, 0.0f);
+      }
+      _Float16 a, b;
+      x2_split(ok ? t * s : 0.0f, a, b);
+      h[e] = a;
+      l[e] = b;
+    }
+    *reinterpret_cast<f16x4*>(hp) = h;
+    *reinterpret_cast<f16x4*>(lp) = l;
+  };
+  auto load_stage = [&](int64_t m_base) __attribute__((always_inline)) {
+    pok = qok = 0;
+#pragma unroll
+    for (int i = 0; i < PI; ++i) rp[i] = raw_row(P, psa, m_base + pr + RPI * i, ptap, pch, pin, pok, i);
+#pragma unroll
+    for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+  };
+  auto store_stage = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PI; ++i)
+      put(rp[i], (pok >> i) & 1u, psa, psc, psh, sp, &Ps[buf][0][pr + RPI * i][pc * 4], &Ps[buf][1][pr + RPI * i][pc * 4]);
+#pragma unroll
+    for (int i = 0; i < PJ; ++i)
+      put(rq[i], (qok >> i) & 1u, qsa, qsc, qsh, sq, &Qs[buf][0][qr + RPJ * i][qc * 4], &Qs[buf][1][qr + RPJ * i][qc * 4]);
+  };
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr8 = [&](const _Float16* p0, const _Float16* p1) __attribute__((always_inline)) {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
+
+  const int64_t nst = me > mb ? (me - mb + KM - 1) / KM : 0;
+  if (nst > 0) {
+    load_stage(mb);
+    store_stage(0);
+    __syncthreads();
+  }
+  for (int64_t st = 0; st < nst; ++st) {
+    const int buf = (int)(st & 1);
+    if (st + 1 < nst) load_stage(mb + (st + 1) * KM);
+#pragma unroll
+    for (int ks = 0; ks < KM / 16; ++ks) {
+      const int row = 16 * ks + 8 * half + q4;
+      f16x8 ah[MT], al[MT], bh[NT], bl[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) {
+        const int col = wi * WI + a * 32 + 16 * grp_hi + 4 * p4;
+        ah[a] = tr8(&Ps[buf][0][row][col], &Ps[buf][0][row + 4][col]);
+        al[a] = tr8(&Ps[buf][1][row][col], &Ps[buf][1][row + 4][col]);
+      }
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const int col = wj * WJ + b * 32 + 16 * grp_hi + 4 * p4;
+        bh[b] = tr8(&Qs[buf][0][row][col], &Qs[buf][0][row + 4][col]);
+        bl[b] = tr8(&Qs[buf][1][row][col], &Qs[buf][1][row + 4][col]);
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (st + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // unscale: column i of P and column j of Q carry their sources' scales
+  auto col_unscale = [&](const GatherArg& g, int k, const float* a0, const float* a1) -> float {
+    int c = k % g.Ctot;
+    const bool s1 = g.nsrc > 1 && c >= g.src[0].C;
+    float u;
+    x2_scale((s1 ? a1 : a0)[0], &u);
+    return u;
+  };
+#pragma unroll
+  for (int b = 0; b < NT; ++b) {
+    const int j = j0 + wj * WJ + b * 32 + l32;
+    const float uq = col_unscale(Q, min(j, Q.K - 1), amax_q0, amax_q1);
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + wi * WI + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const float up = col_unscale(P, min(i, P.K - 1), amax_p0, amax_p1);
+        ws[split * ws_stride + (int64_t)i * ldo + j] = acc[a][b][r] * (up * uq);
+      }
+    }
+  }
+}
+
 // =========================================================================== gemm_wgrad (bf16)
 // Same contraction with v_mfma_f32_32x32x16_bf16. The LDS tiles stay in their natural gathered
 // layout [pixel m][column] (coalesced staging); the MFMA operands need 8 consecutive m per
@@ -1346,6 +1521,66 @@ extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_g
   hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
                      (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
   return check_launch("conv3x3_wgrad_x2");
+}
+
+// generic fp32 weight gradient on split-fp16 operands (gemm_wgrad_x2_kernel + the fixed-order split
+// reduction into the reference layout)
+static int plan_wgrad_gx2(const selunet_gather* p, const selunet_gather* q, WgradPlan& w) {
+  if (int rc = plan_wgrad(p, q, SELUNET_F32, w)) return rc;
+  SELUNET_REQUIRE(!w.gp.small && !w.gq.small && w.gp.K % 64 == 0 && w.gq.K % 64 == 0,
+                  "gemm_wgrad_x2: vector gathers with K_p, K_q multiples of 64 (got %d, %d)", w.gp.K, w.gq.K);
+  const int bi = w.ni % 128 == 0 ? 128 : 64;
+  w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
+  return 0;
+}
+
+extern "C" int64_t selunet_gemm_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q) {
+  WgradPlan w;
+  if (plan_wgrad_gx2(p, q, w)) return -1;
+  return w.splits * (int64_t)w.ni * w.nj_pad * 4;
+}
+
+extern "C" int selunet_gemm_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                     int32_t layout, float* out, const float* amax_p0, const float* amax_p1,
+                                     const float* amax_q0, const float* amax_q1, void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad_gx2(p, q, w)) return rc;
+  SELUNET_REQUIRE(out != nullptr && (layout == WG_CONV3X3 || layout == WG_CONVT), "gemm_wgrad_x2: bad arguments");
+  SELUNET_REQUIRE(w.gq.K % (layout == WG_CONV3X3 ? 9 : 4) == 0, "gemm_wgrad_x2: K_q = %d is not a multiple of %d",
+                  w.gq.K, layout == WG_CONV3X3 ? 9 : 4);
+  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  SELUNET_REQUIRE(ws != nullptr && ws_bytes >= need, "gemm_wgrad_x2: workspace of %lld bytes needed", (long long)need);
+  SELUNET_REQUIRE(amax_p0 && amax_q0 && (p->nsrc == 1 || amax_p1) && (q->nsrc == 1 || amax_q1),
+                  "gemm_wgrad_x2: every operand source needs its range word");
+  hipStream_t st = as_stream(stream);
+  const int bi = w.ni % 128 == 0 ? 128 : 64;
+  const int tiles_j = w.nj_pad / w.bj, tiles = (w.ni / bi) * tiles_j;
+  int64_t mchunk;
+  wgrad_splits(w.gp.M, tiles, &mchunk);
+  const unsigned blocks = (unsigned)(tiles * w.splits);
+  const int64_t stride = (int64_t)w.ni * w.nj_pad;
+  if (bi == 128 && w.bj == 128)
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<128, 128>), dim3(blocks), dim3(256), 0, st, w.gp, w.gq, w.nj_pad, mchunk,
+                       tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  else if (w.bj == 128)
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<64, 128>), dim3(blocks), dim3(256), 0, st, w.gp, w.gq, w.nj_pad, mchunk,
+                       tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  else if (bi == 128)
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<128, 64>), dim3(blocks), dim3(256), 0, st, w.gp, w.gq, w.nj_pad, mchunk,
+                       tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  else
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<64, 64>), dim3(blocks), dim3(256), 0, st, w.gp, w.gq, w.nj_pad, mchunk,
+                       tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  if (int rc = check_launch("gemm_wgrad_x2")) return rc;
+  const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
+  const unsigned rblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
+  if (layout == WG_CONV3X3)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(rblocks), dim3(64), 0, st, ws, w.splits, stride, w.ni,
+                       w.nj_pad, w.gq.K, out);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONVT>, dim3(rblocks), dim3(64), 0, st, ws, w.splits, stride, w.ni,
+                       w.nj_pad, w.gq.K, out);
+  return check_launch("gemm_wgrad_x2");
 }
 
 // leading dimension of the packed wgrad output for a Q operand with kq columns

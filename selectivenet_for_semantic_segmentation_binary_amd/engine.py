@@ -597,7 +597,14 @@ class Engine:
         ld = K.query("selunet_wgrad_ld", 4 * co)
         gp = K.gather(n, h, w, 1, prev.src())
         gq = K.gather(n, h, w, 4, K.source(du.t, co))
-        self._wgrad_param(gp, gq, K.WG_CONVT, ci, ld, G[f"{name}.weight"])
+        duw = self._word(ctx, "du:decoder_layer_" + name[-1] + "_2") if wp.mode == "x2" else None
+        wsb = K.query("selunet_gemm_wgrad_x2_ws_bytes", gp, gq) if duw is not None else -1
+        if wsb > 0:  # split-fp16 weight gradient (unpool k feeds decoder_layer_k_2)
+            ws = K.keep(torch.empty(wsb // 4, dtype=torch.float32, device=dev))
+            K.call("selunet_gemm_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.WG_CONVT, K.ptr(G[f"{name}.weight"]),
+                   K.ptr(prev.amax), None, K.ptr(duw), None, self.stream)
+        else:
+            self._wgrad_param(gp, gq, K.WG_CONVT, ci, ld, G[f"{name}.weight"])
         K.marker(("grads", name))
         dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))
@@ -606,7 +613,6 @@ class Engine:
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = bnb_for(prev, slab)
         if wp.mode == "x2":
-            duw = self._word(ctx, "du:decoder_layer_" + name[-1] + "_2")  # unpool k feeds decoder_layer_k_2
             K.call("selunet_gemm_gather_x2", ga, K.ptr(wd), ci, 4 * co, ep, K.ptr(duw), None, self.stream)
         else:
             K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)

@@ -330,3 +330,34 @@ def test_x2_convT_fwd_dgrad(cin, cout, gwgs, gather_wgs):
     torch.cuda.synchronize()
     assert rel(nchw(da.cpu(), n, h, w), ga) < TOL
     check_bnb_sums(slab, da, yprev, sc, sh, mean, invstd)
+
+
+@pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64), (256, 128)])
+def test_x2_convT_wgrad(cin, cout):
+    """ConvTranspose2d weight gradient through selunet_gemm_wgrad_x2 (split partials reduced into the
+    [ci][co][2][2] layout) against torch in fp64; bit-reproducible."""
+    n, h, w = 2, 13, 18
+    x = gen(n, cin, h, w, seed=13)
+    s, t = bn_fold(cin, 30)
+    a = torch.relu(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1)).double()
+    wt = gen(cin, cout, 2, 2, seed=14, scale=0.05).double().requires_grad_()
+    y = F.conv_transpose2d(a, wt, None, stride=2)
+    dy = gen(*y.shape, seed=16) * 1e-8
+    (gw,) = torch.autograd.grad(y, (wt,), dy.double())
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    xd, sd, td, dud = d(nhwc(x)), d(s), d(t), d(nhwc(dy))
+    amp, amq = word(a.abs().max()), word(dy.abs().max())
+    gp = K.gather(n, h, w, 1, K.source(xd, cin, sd, td))
+    gq = K.gather(n, h, w, 4, K.source(dud, cout))
+    wsb = K.query("selunet_gemm_wgrad_x2_ws_bytes", gp, gq)
+    assert wsb > 0
+    ws = torch.empty(wsb // 4, device=DEV)
+    outs = []
+    for _ in range(2):
+        out = torch.full((cin, cout, 2, 2), float("nan"), device=DEV)
+        K.call("selunet_gemm_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.WG_CONVT, K.ptr(out), K.ptr(amp), None, K.ptr(amq),
+               None, K.stream_ptr())
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert rel(outs[0].cpu(), gw) < TOL
+    assert torch.equal(outs[0], outs[1])
