@@ -429,6 +429,16 @@ int selunet_selective_finalize(const double* sums, double p_global, float lamb,
 int selunet_selective_bwd(const float* out, const float* sel, const float* target, int64_t p,
                           const float* state, float lamb, const float* g_loss,
                           const float* g_coverage, float* d_out, float* d_sel, void* stream);
+/* hard_selection=True (selective_loss.py:74-77): the risk numerator weights pixels by the detached
+ * hard selection [sigmoid(g) > 0.5] (slab column 1 = sum ell*[sigmoid(g) > 0.5]; column 0 stays
+ * sum sigmoid(g), the coverage); finalized by selunet_selective_finalize. Selection and coverage are
+ * detached in the reference, so the backward writes d_sel = 0 and
+ * d_out = g_loss * [sigmoid(g) > 0.5] * (sigmoid(x) - t) / sum sigmoid(g). */
+int selunet_selective_partials_hard(const float* out, const float* sel, const float* target,
+                                    int64_t p, float* slab, void* stream);
+int selunet_selective_bwd_hard(const float* out, const float* sel, const float* target, int64_t p,
+                               const float* state, const float* g_loss, float* d_out, float* d_sel,
+                               void* stream);
 /* BCEWithLogitsLoss() mean (train.py:78): slab [selunet_loss_slab_rows(P)][1]. */
 int selunet_bce_partials(const float* logit, const float* target, int64_t p, float* slab,
                          void* stream);
@@ -436,7 +446,8 @@ int selunet_bce_finalize(const double* sums, double p_global, float* loss, void*
 int selunet_bce_bwd(const float* logit, const float* target, int64_t p, double p_global,
                     const float* g_loss, float* d_logit, void* stream);
 /* Cross-entropy forms (CE `UNet`, n_cls = C <= 8): logits NCHW fp32 [N][C][hw], selection NCHW
- * [N][2][hw], target int64 class indices [N][hw] (values outside [0, C) are clamped).
+ * [N][2][hw], target int64 class indices [N][hw] (a value outside [0, C) makes that pixel's loss
+ * term and gradients NaN, as torch rejects it).
  * calc_selective_risk_image (selective_loss.py:24-56): s = softmax(selection)[:, 1],
  * ell = -log_softmax(output)[target]; partials slab [selunet_loss_slab_rows(N*hw)][2] = sum s,
  * sum ell*s — finalized by selunet_selective_finalize exactly as the BCE form. */
@@ -445,6 +456,12 @@ int selunet_ce_selective_partials(const float* out, const float* sel, const int6
 int selunet_ce_selective_bwd(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
                              int64_t hw, const float* state, float lamb, const float* g_loss,
                              const float* g_coverage, float* d_out, float* d_sel, void* stream);
+/* hard_selection=True of the CE form (selective_loss.py:43-48), as the _hard BCE entry points. */
+int selunet_ce_selective_partials_hard(const float* out, const float* sel, const int64_t* target, int64_t n,
+                                       int32_t c, int64_t hw, float* slab, void* stream);
+int selunet_ce_selective_bwd_hard(const float* out, const float* sel, const int64_t* target, int64_t n,
+                                  int32_t c, int64_t hw, const float* state, const float* g_loss,
+                                  float* d_out, float* d_sel, void* stream);
 /* torch.nn.CrossEntropyLoss() mean (train.py:80): slab [selunet_loss_slab_rows(N*hw)][1] = sum ell,
  * finalized by selunet_bce_finalize (sum / P). */
 int selunet_ce_partials(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw,

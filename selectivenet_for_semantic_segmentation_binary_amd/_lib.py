@@ -138,12 +138,16 @@ SIGNATURES = {
                                            ctypes.POINTER(BnBwdStats), c_int32, P]),
     "selunet_ce_selective_partials": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, P]),
     "selunet_ce_selective_bwd": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, c_float, P, P, P, P, P]),
+    "selunet_ce_selective_partials_hard": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, P]),
+    "selunet_ce_selective_bwd_hard": (c_int32, [P, P, P, c_int64, c_int32, c_int64, P, P, P, P, P]),
     "selunet_ce_partials": (c_int32, [P, P, c_int64, c_int32, c_int64, P, P]),
     "selunet_ce_bwd": (c_int32, [P, P, c_int64, c_int32, c_int64, c_double, P, P, P]),
     "selunet_loss_slab_rows": (c_int64, [c_int64]),
     "selunet_selective_partials": (c_int32, [P, P, P, c_int64, P, P]),
     "selunet_selective_finalize": (c_int32, [P, c_double, c_float, c_float, P, P, P, P]),
     "selunet_selective_bwd": (c_int32, [P, P, P, c_int64, P, c_float, P, P, P, P, P]),
+    "selunet_selective_partials_hard": (c_int32, [P, P, P, c_int64, P, P]),
+    "selunet_selective_bwd_hard": (c_int32, [P, P, P, c_int64, P, P, P, P, P]),
     "selunet_bce_partials": (c_int32, [P, P, c_int64, P, P]),
     "selunet_bce_finalize": (c_int32, [P, c_double, P, P]),
     "selunet_bce_bwd": (c_int32, [P, P, c_int64, c_double, P, P, P]),

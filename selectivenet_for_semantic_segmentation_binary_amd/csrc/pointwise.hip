@@ -896,6 +896,9 @@ __device__ inline void block_sum_store(float (&v)[NV], float* dst) {
   }
 }
 
+// HARD (hard_selection=True, selective_loss.py:74-77): the risk numerator weights each pixel by the
+// detached hard selection [sigmoid(g) > 0.5] instead of sigmoid(g); the coverage stays the soft mean.
+template <bool HARD>
 __global__ void selective_partials_kernel(const float* __restrict__ out, const float* __restrict__ sel,
                                           const float* __restrict__ tgt, int64_t P, float* slab) {
   const int64_t rows = gridDim.x;
@@ -907,7 +910,7 @@ __global__ void selective_partials_kernel(const float* __restrict__ out, const f
     const float x = out[i], t = tgt[i];
     const float ell = t * softplusf_(-x) + (1.0f - t) * softplusf_(x);
     acc[0] += s;
-    acc[1] += ell * s;
+    acc[1] += ell * (HARD ? (s > 0.5f ? 1.0f : 0.0f) : s);
   }
   block_sum_store<2>(acc, slab + blockIdx.x * 2);
 }
@@ -926,6 +929,9 @@ __global__ void selective_finalize_kernel(const double* sums, double P, float la
   state[3] = (float)P;
 }
 
+// HARD: selection and coverage are detached (selective_loss.py:75-76), so d_sel = 0 and the
+// output gradient carries the hard weight over the (constant) soft selection sum.
+template <bool HARD>
 __global__ void selective_bwd_kernel(const float* __restrict__ out, const float* __restrict__ sel,
                                      const float* __restrict__ tgt, int64_t P, const float* state, float lamb,
                                      const float* g_loss, const float* g_cov, float* d_out, float* d_sel) {
@@ -938,9 +944,14 @@ __global__ void selective_bwd_kernel(const float* __restrict__ out, const float*
     const float s = sigmoidf_(sel[i]);
     const float x = out[i], t = tgt[i];
     const float px = sigmoidf_(x);
-    const float ell = t * softplusf_(-x) + (1.0f - t) * softplusf_(x);
-    d_out[i] = gl * s * (px - t) * inv_s0;
-    d_sel[i] = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
+    if constexpr (HARD) {
+      d_out[i] = gl * (s > 0.5f ? 1.0f : 0.0f) * (px - t) * inv_s0;
+      d_sel[i] = 0.0f;
+    } else {
+      const float ell = t * softplusf_(-x) + (1.0f - t) * softplusf_(x);
+      d_out[i] = gl * s * (px - t) * inv_s0;
+      d_sel[i] = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
+    }
   }
 }
 
@@ -1116,6 +1127,7 @@ __device__ __forceinline__ int ce_target(const int64_t* tgt, int64_t i, int C) {
 }
 __device__ __forceinline__ float ce_onehot(int c, int t) { return t < 0 ? __builtin_nanf("") : (c == t ? 1.0f : 0.0f); }
 
+template <bool HARD>
 __global__ void ce_selective_partials_kernel(const float* __restrict__ out, const float* __restrict__ sel,
                                              const int64_t* __restrict__ tgt, int64_t P, int C, int64_t hw,
                                              float* slab) {
@@ -1129,11 +1141,12 @@ __global__ void ce_selective_partials_kernel(const float* __restrict__ out, cons
     float e[8], inv_se;
     const float ell = ce_pixel(out, img * C * hw + q, hw, C, ce_target(tgt, i, C), e, inv_se);
     acc[0] += s;
-    acc[1] += ell * s;
+    acc[1] += ell * (HARD ? (s > 0.5f ? 1.0f : 0.0f) : s);
   }
   block_sum_store<2>(acc, slab + blockIdx.x * 2);
 }
 
+template <bool HARD>
 __global__ void ce_selective_bwd_kernel(const float* __restrict__ out, const float* __restrict__ sel,
                                         const int64_t* __restrict__ tgt, int64_t P, int C, int64_t hw,
                                         const float* state, float lamb, const float* g_loss, const float* g_cov,
@@ -1151,11 +1164,11 @@ __global__ void ce_selective_bwd_kernel(const float* __restrict__ out, const flo
     const int64_t base = img * C * hw + q;
     float e[8], inv_se;
     const float ell = ce_pixel(out, base, hw, C, t, e, inv_se);
-    const float k = gl * s * inv_s0;
+    const float k = gl * (HARD ? (s > 0.5f ? 1.0f : 0.0f) : s) * inv_s0;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
       if (c < C) d_out[base + c * hw] = k * (e[c] * inv_se - ce_onehot(c, t));
-    const float ds = s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
+    const float ds = HARD ? 0.0f : s * (1.0f - s) * (gl * (ell - R) * inv_s0 + cterm);
     d_sel[s1i] = ds;
     d_sel[s0i] = -ds;
   }
@@ -1593,12 +1606,20 @@ int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float*
 
 int64_t selunet_loss_slab_rows(int64_t p) { return loss_slab_rows(p); }
 
+static int selective_partials(bool hard, const float* out, const float* sel, const float* target, int64_t p,
+                              float* slab, void* stream) {
+  SELUNET_REQUIRE(out && sel && target && slab && p > 0, "selective_partials: bad arguments");
+  hipLaunchKernelGGL(hard ? selective_partials_kernel<true> : selective_partials_kernel<false>,
+                     dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream), out, sel, target, p, slab);
+  return check_launch("selective_partials");
+}
 int selunet_selective_partials(const float* out, const float* sel, const float* target, int64_t p, float* slab,
                                void* stream) {
-  SELUNET_REQUIRE(out && sel && target && slab && p > 0, "selective_partials: bad arguments");
-  hipLaunchKernelGGL(selective_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream),
-                     out, sel, target, p, slab);
-  return check_launch("selective_partials");
+  return selective_partials(false, out, sel, target, p, slab, stream);
+}
+int selunet_selective_partials_hard(const float* out, const float* sel, const float* target, int64_t p, float* slab,
+                                    void* stream) {
+  return selective_partials(true, out, sel, target, p, slab, stream);
 }
 
 int selunet_selective_finalize(const double* sums, double p_global, float lamb, float target_coverage, float* loss,
@@ -1609,13 +1630,23 @@ int selunet_selective_finalize(const double* sums, double p_global, float lamb, 
   return check_launch("selective_finalize");
 }
 
+static int selective_bwd(bool hard, const float* out, const float* sel, const float* target, int64_t p,
+                         const float* state, float lamb, const float* g_loss, const float* g_coverage, float* d_out,
+                         float* d_sel, void* stream) {
+  SELUNET_REQUIRE(out && sel && target && state && d_out && d_sel && p > 0, "selective_bwd: bad arguments");
+  hipLaunchKernelGGL(hard ? selective_bwd_kernel<true> : selective_bwd_kernel<false>, dim3(grid_for(p, 8192)),
+                     dim3(TPB), 0, as_stream(stream), out, sel, target, p, state, lamb, g_loss, g_coverage, d_out,
+                     d_sel);
+  return check_launch("selective_bwd");
+}
 int selunet_selective_bwd(const float* out, const float* sel, const float* target, int64_t p, const float* state,
                           float lamb, const float* g_loss, const float* g_coverage, float* d_out, float* d_sel,
                           void* stream) {
-  SELUNET_REQUIRE(out && sel && target && state && d_out && d_sel && p > 0, "selective_bwd: bad arguments");
-  hipLaunchKernelGGL(selective_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), out, sel, target,
-                     p, state, lamb, g_loss, g_coverage, d_out, d_sel);
-  return check_launch("selective_bwd");
+  return selective_bwd(false, out, sel, target, p, state, lamb, g_loss, g_coverage, d_out, d_sel, stream);
+}
+int selunet_selective_bwd_hard(const float* out, const float* sel, const float* target, int64_t p,
+                               const float* state, const float* g_loss, float* d_out, float* d_sel, void* stream) {
+  return selective_bwd(true, out, sel, target, p, state, 0.0f, g_loss, nullptr, d_out, d_sel, stream);
 }
 
 int selunet_bce_partials(const float* logit, const float* target, int64_t p, float* slab, void* stream) {
@@ -1702,25 +1733,45 @@ int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const
   return check_launch("heads_bwd_planes");
 }
 
-int selunet_ce_selective_partials(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
-                                  int64_t hw, float* slab, void* stream) {
+static int ce_selective_partials(bool hard, const float* out, const float* sel, const int64_t* target, int64_t n,
+                                 int32_t c, int64_t hw, float* slab, void* stream) {
   SELUNET_REQUIRE(out && sel && target && slab && n > 0 && hw > 0 && c >= 1 && c <= 8,
                   "ce_selective_partials: bad arguments (n_cls must be 1..8)");
   const int64_t p = n * hw;
-  hipLaunchKernelGGL(ce_selective_partials_kernel, dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream),
-                     out, sel, target, p, c, hw, slab);
+  hipLaunchKernelGGL(hard ? ce_selective_partials_kernel<true> : ce_selective_partials_kernel<false>,
+                     dim3((unsigned)loss_slab_rows(p)), dim3(TPB), 0, as_stream(stream), out, sel, target, p, c, hw,
+                     slab);
   return check_launch("ce_selective_partials");
 }
+int selunet_ce_selective_partials(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                                  int64_t hw, float* slab, void* stream) {
+  return ce_selective_partials(false, out, sel, target, n, c, hw, slab, stream);
+}
+int selunet_ce_selective_partials_hard(const float* out, const float* sel, const int64_t* target, int64_t n,
+                                       int32_t c, int64_t hw, float* slab, void* stream) {
+  return ce_selective_partials(true, out, sel, target, n, c, hw, slab, stream);
+}
 
-int selunet_ce_selective_bwd(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
-                             int64_t hw, const float* state, float lamb, const float* g_loss, const float* g_coverage,
-                             float* d_out, float* d_sel, void* stream) {
+static int ce_selective_bwd(bool hard, const float* out, const float* sel, const int64_t* target, int64_t n,
+                            int32_t c, int64_t hw, const float* state, float lamb, const float* g_loss,
+                            const float* g_coverage, float* d_out, float* d_sel, void* stream) {
   SELUNET_REQUIRE(out && sel && target && state && d_out && d_sel && n > 0 && hw > 0 && c >= 1 && c <= 8,
                   "ce_selective_bwd: bad arguments");
   const int64_t p = n * hw;
-  hipLaunchKernelGGL(ce_selective_bwd_kernel, dim3(grid_for(p, 8192)), dim3(TPB), 0, as_stream(stream), out, sel,
-                     target, p, c, hw, state, lamb, g_loss, g_coverage, d_out, d_sel);
+  hipLaunchKernelGGL(hard ? ce_selective_bwd_kernel<true> : ce_selective_bwd_kernel<false>, dim3(grid_for(p, 8192)),
+                     dim3(TPB), 0, as_stream(stream), out, sel, target, p, c, hw, state, lamb, g_loss, g_coverage,
+                     d_out, d_sel);
   return check_launch("ce_selective_bwd");
+}
+int selunet_ce_selective_bwd(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                             int64_t hw, const float* state, float lamb, const float* g_loss, const float* g_coverage,
+                             float* d_out, float* d_sel, void* stream) {
+  return ce_selective_bwd(false, out, sel, target, n, c, hw, state, lamb, g_loss, g_coverage, d_out, d_sel, stream);
+}
+int selunet_ce_selective_bwd_hard(const float* out, const float* sel, const int64_t* target, int64_t n, int32_t c,
+                                  int64_t hw, const float* state, const float* g_loss, float* d_out, float* d_sel,
+                                  void* stream) {
+  return ce_selective_bwd(true, out, sel, target, n, c, hw, state, 0.0f, g_loss, nullptr, d_out, d_sel, stream);
 }
 
 int selunet_ce_partials(const float* logit, const int64_t* target, int64_t n, int32_t c, int64_t hw, float* slab,

@@ -69,13 +69,13 @@ def global_count(shape) -> float:
 
 class _SelectiveRiskB(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, output, selection, target, target_coverage, lamb):
+    def forward(ctx, output, selection, target, target_coverage, lamb, hard=False):
         p = output.numel()
         dev = output.device
         rows = K.query("selunet_loss_slab_rows", p)
         slab = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        K.call("selunet_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), p, K.ptr(slab),
-               K.stream_ptr())
+        K.call("selunet_selective_partials_hard" if hard else "selunet_selective_partials", K.ptr(output),
+               K.ptr(selection), K.ptr(target), p, K.ptr(slab), K.stream_ptr())
         sums = _reduced_sums(slab, rows, 2)
         p_global = global_count(output.shape)
         loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -84,7 +84,9 @@ class _SelectiveRiskB(torch.autograd.Function):
         K.call("selunet_selective_finalize", K.ptr(sums), p_global, float(lamb), float(target_coverage), K.ptr(loss),
                K.ptr(coverage), K.ptr(state), K.stream_ptr())
         ctx.save_for_backward(output, selection, target, state)
-        ctx.lamb = float(lamb)
+        ctx.lamb, ctx.hard = float(lamb), hard
+        if hard:
+            ctx.mark_non_differentiable(coverage)  # coverage.clone().detach(), selective_loss.py:76
         return loss, coverage
 
     @staticmethod
@@ -94,21 +96,25 @@ class _SelectiveRiskB(torch.autograd.Function):
         d_sel = torch.empty_like(selection)
         gl = g_loss.contiguous().float() if g_loss is not None else None
         gc = g_cov.contiguous().float() if g_cov is not None else None
+        if ctx.hard:  # selection detached: no gradient reaches it (d_sel is written as zeros)
+            K.call("selunet_selective_bwd_hard", K.ptr(output), K.ptr(selection), K.ptr(target), output.numel(),
+                   K.ptr(state), K.ptr(gl), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
+            return d_out, None, None, None, None, None
         K.call("selunet_selective_bwd", K.ptr(output), K.ptr(selection), K.ptr(target), output.numel(), K.ptr(state),
                ctx.lamb, K.ptr(gl), K.ptr(gc), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
-        return d_out, d_sel, None, None, None
+        return d_out, d_sel, None, None, None, None
 
 
 def calc_selective_risk_image_b(output, selection, target, target_coverage=0.8, lamb=8, hard_selection=False):
-    """selective_loss.py:58-85 (BCE-with-logits selective risk). output/selection/target: (N, H, W)."""
-    if hard_selection:
-        raise NotImplementedError("hard_selection=True (selective_loss.py:74-77) is not on the training path "
-                                  "(train.py:196 never sets it) and is not implemented on the MI355X path")
+    """selective_loss.py:58-85 (BCE-with-logits selective risk). output/selection/target: (N, H, W).
+
+    hard_selection=True (selective_loss.py:74-77): the risk's selection weight is the detached
+    [sigmoid(g) > 0.5], the coverage the detached soft mean — the loss then reaches `output` only."""
     if output.shape != selection.shape or output.shape != target.shape:
         raise ValueError(f"shape mismatch: output {tuple(output.shape)}, selection {tuple(selection.shape)}, "
                          f"target {tuple(target.shape)}")
     o, s, t = _check(output, "output"), _check(selection, "selection"), _check(target, "target")
-    return _SelectiveRiskB.apply(o, s, t, target_coverage, lamb)
+    return _SelectiveRiskB.apply(o, s, t, target_coverage, lamb, bool(hard_selection))
 
 
 class _BCEWithLogitsMean(torch.autograd.Function):
@@ -170,13 +176,13 @@ def _check_target_ce(target, logits):
 
 class _SelectiveRiskCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, output, selection, target, target_coverage, lamb):
+    def forward(ctx, output, selection, target, target_coverage, lamb, hard=False):
         n, c, h, w = output.shape
         hw, p = h * w, n * h * w
         dev = output.device
         rows = K.query("selunet_loss_slab_rows", p)
         slab = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        K.call("selunet_ce_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, hw, K.ptr(slab),
+        K.call("selunet_ce_selective_partials_hard" if hard else "selunet_ce_selective_partials", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, hw, K.ptr(slab),
                K.stream_ptr())
         sums = _reduced_sums(slab, rows, 2)
         p_global = global_count((n, h, w))
@@ -186,7 +192,9 @@ class _SelectiveRiskCE(torch.autograd.Function):
         K.call("selunet_selective_finalize", K.ptr(sums), p_global, float(lamb), float(target_coverage), K.ptr(loss),
                K.ptr(coverage), K.ptr(state), K.stream_ptr())
         ctx.save_for_backward(output, selection, target, state)
-        ctx.lamb = float(lamb)
+        ctx.lamb, ctx.hard = float(lamb), hard
+        if hard:
+            ctx.mark_non_differentiable(coverage)  # selective_loss.py:47
         return loss, coverage
 
     @staticmethod
@@ -197,9 +205,13 @@ class _SelectiveRiskCE(torch.autograd.Function):
         d_sel = torch.empty_like(selection)
         gl = g_loss.contiguous().float() if g_loss is not None else None
         gc = g_cov.contiguous().float() if g_cov is not None else None
+        if ctx.hard:
+            K.call("selunet_ce_selective_bwd_hard", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, h * w,
+                   K.ptr(state), K.ptr(gl), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
+            return d_out, None, None, None, None, None
         K.call("selunet_ce_selective_bwd", K.ptr(output), K.ptr(selection), K.ptr(target), n, c, h * w, K.ptr(state),
                ctx.lamb, K.ptr(gl), K.ptr(gc), K.ptr(d_out), K.ptr(d_sel), K.stream_ptr())
-        return d_out, d_sel, None, None, None
+        return d_out, d_sel, None, None, None, None
 
 
 def calc_selective_risk_image(output, selection, target, target_coverage=0.8, lamb=8, hard_selection=False):
@@ -210,10 +222,8 @@ def calc_selective_risk_image(output, selection, target, target_coverage=0.8, la
         risk = -mean(sum_c log_softmax(output, 1) * onehot(target) * s) / coverage
         loss = risk + lamb * max(target_coverage - coverage, 0)^2
 
-    (the reference's one-hot target (N, C, H, W) form is accepted too and reduced to indices)."""
-    if hard_selection:
-        raise NotImplementedError("hard_selection=True (selective_loss.py:43-48) is not on the training path "
-                                  "and is not implemented on the MI355X path")
+    (the reference's one-hot target (N, C, H, W) form is accepted too and reduced to indices).
+    hard_selection=True (selective_loss.py:43-48): detached [s > 0.5] weights, detached coverage."""
     if output.dim() != 4 or selection.dim() != 4 or selection.shape[1] != 2 or \
             selection.shape[0] != output.shape[0] or selection.shape[2:] != output.shape[2:]:
         raise ValueError(f"expected output (N, C, H, W) and selection (N, 2, H, W); got {tuple(output.shape)}, "
@@ -221,7 +231,7 @@ def calc_selective_risk_image(output, selection, target, target_coverage=0.8, la
     if target.dim() == 4:  # one-hot (N, C, H, W) as selective_loss.py:36-37 builds it
         target = target.argmax(1)
     o, s = _check(output, "output"), _check(selection, "selection")
-    return _SelectiveRiskCE.apply(o, s, _check_target_ce(target, o), target_coverage, lamb)
+    return _SelectiveRiskCE.apply(o, s, _check_target_ce(target, o), target_coverage, lamb, bool(hard_selection))
 
 
 class _CrossEntropyMean(torch.autograd.Function):

@@ -322,6 +322,52 @@ def loss_cases():
     print(f"wrote {path}")
 
 
+def hard_cases():
+    """hard_selection=True of calc_selective_risk_image_b (selective_loss.py:74-77) and of
+    calc_selective_risk_image (selective_loss.py:43-48): loss, coverage and the output gradient (the
+    selection gets none). Selection logits are kept at |g| >= 1e-3 so no pixel sits on the 0.5 cut."""
+    out = {}
+    rng = np.random.Generator(np.random.PCG64(11))
+    cases = []
+
+    def away(a):
+        return np.where(np.abs(a) < 1e-3, np.float32(1e-3) * np.sign(a + 1e-9), a).astype(np.float32)
+
+    for i, (scale, shape, sel_mu) in enumerate([(1.0, (2, 8, 8), 0.5), (3.0, (2, 16, 16), 0.0),
+                                                 (1.0, (2, 8, 8), -2.0)]):
+        o = rng.normal(0, scale, shape).astype(np.float32)
+        s = away(rng.normal(sel_mu, scale, shape).astype(np.float32))
+        t = (rng.random(shape) > 0.5).astype(np.float32)
+        key = f"b{i}"
+        ot, st = torch.tensor(o, requires_grad=True), torch.tensor(s, requires_grad=True)
+        loss, cov = ref_loss.calc_selective_risk_image_b(ot, st, torch.tensor(t), lamb=2, hard_selection=True)
+        g = torch.autograd.grad(loss, (ot, st), allow_unused=True)
+        assert g[1] is None and not cov.requires_grad
+        out.update({key + "/output": o, key + "/selection": s, key + "/target": t,
+                    key + "/loss": np.float64(loss.item()), key + "/coverage": np.float64(cov.item()),
+                    key + "/g_output": g[0].numpy()})
+        cases.append(key)
+    for i, (c, shape) in enumerate([(2, (2, 8, 8)), (3, (1, 16, 16))]):
+        n, h, w = shape
+        o = rng.normal(0, 1.5, (n, c, h, w)).astype(np.float32)
+        s = rng.normal(0, 1.0, (n, 2, h, w)).astype(np.float32)
+        s[:, 1] = s[:, 0] + away(s[:, 1] - s[:, 0])
+        t = rng.integers(0, c, (n, h, w)).astype(np.int64)
+        key = f"ce{i}"
+        ot, st = torch.tensor(o, requires_grad=True), torch.tensor(s, requires_grad=True)
+        loss, cov = ref_loss.calc_selective_risk_image(ot, st, torch.tensor(t), lamb=2, hard_selection=True)
+        g = torch.autograd.grad(loss, (ot, st), allow_unused=True)
+        assert g[1] is None
+        out.update({key + "/output": o, key + "/selection": s, key + "/target": t,
+                    key + "/loss": np.float64(loss.item()), key + "/coverage": np.float64(cov.item()),
+                    key + "/g_output": g[0].numpy()})
+        cases.append(key)
+    out["cases"] = np.array(cases)
+    path = os.path.join(HERE, "loss_cases_hard.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}")
+
+
 def bisect_threshold(pred_fn):
     """Smallest positive fp32 logit x with pred_fn(x) == 1 (bisection over fp32 bit patterns)."""
     lo, hi = 0, np.float32(1.0).view(np.int32).item()
@@ -745,12 +791,16 @@ if __name__ == "__main__":
     if sys.argv[1:2] == ["miou_spread"]:
         miou_spread(int(sys.argv[2]) if len(sys.argv) > 2 else 8)
         sys.exit(0)
+    if sys.argv[1:] == ["hard"]:
+        hard_cases()
+        sys.exit(0)
     if sys.argv[1:] == ["ce"]:
         ce_step_fixture("step_ce_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
         ce_step_fixture("step_ce_nosel_n2_32.npz", 2, 32, selective=False, steps=1)
         sys.exit(0)
     kats()
     loss_cases()
+    hard_cases()
     step_fixture("step_sel_n2_64.npz", 2, 64, selective=True, lamb=2, steps=2)
     step_fixture("step_nosel_n2_64.npz", 2, 64, selective=False, steps=2)
     step_fixture("step_sel_lamb8_n3_32.npz", 3, 32, selective=True, lamb=8, steps=1)

@@ -82,6 +82,25 @@ def test_loss_cases_literal_and_stable():
             assert abs(O.bce_with_logits_mean(o.detach(), t).item() - float(d[f"{case}/bce"])) < 1e-6
 
 
+def test_hard_selection_cases():
+    """hard_selection=True (selective_loss.py:43-48, 74-77) on the reference's own outputs
+    (tests/golden/loss_cases_hard.npz): loss, coverage and the output gradient; none reaches the
+    selection."""
+    d = G.load("loss_cases_hard.npz")
+    for case in d["cases"]:
+        o, s = (torch.tensor(d[f"{case}/{n}"], requires_grad=True) for n in ("output", "selection"))
+        t = torch.tensor(d[f"{case}/target"])
+        if case.startswith("ce"):
+            loss, cov = O.selective_risk_ce_literal(o, s, t, lamb=2, hard_selection=True)
+        else:
+            loss, cov = O.selective_risk_b_stable(o, s, t, lamb=2, hard_selection=True)
+        assert abs(loss.item() - float(d[f"{case}/loss"])) <= 1e-6 * max(1.0, abs(float(d[f"{case}/loss"]))), case
+        assert abs(cov.item() - float(d[f"{case}/coverage"])) < 1e-7 and not cov.requires_grad
+        go, gs = torch.autograd.grad(loss, (o, s), allow_unused=True)
+        assert gs is None
+        assert G.max_rel(go, d[f"{case}/g_output"]) < 1e-5, case
+
+
 def _run_oracle_fixture(fname, loss_form="literal"):
     """Step 0 is compared strictly (1e-4 on grads). Later steps are compared loosely:
     Adam's update is ~lr*sign(g) for |g| >> eps, so an element whose gradient is within
