@@ -450,15 +450,29 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
 #pragma unroll
         for (int a = 0; a < MT; ++a) {
           const unsigned char* p = a_src + (hrow0[a] + tap_off) * AROWB + ((hsw0[a] ^ dy) & 1) * 16;
+#if (SELUNET_ABL & 64)
+          ah[a] = f16x8{} + (_Float16)(t + a);
+          al[a] = f16x8{} + (_Float16)(ks + a);
+#else
           ah[a] = *reinterpret_cast<const f16x8*>(p + ks * 32);
           al[a] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+#endif
         }
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
           const unsigned char* p = b_src + (wn * 64 + b * 32 + l32) * ROWB + half * 16;
+#if (SELUNET_ABL & 64)
+          bh[b] = f16x8{} + (_Float16)(t + b);
+          bl[b] = f16x8{} + (_Float16)(ks + b);
+#else
           bh[b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
           bl[b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+#endif
         }
+#if (SELUNET_ABL & 16)
+        asm volatile("" :: "v"(ah[0]), "v"(al[MT - 1]), "v"(bh[0]), "v"(bl[NT - 1]));
+        continue;
+#endif
 #pragma unroll
         for (int a = 0; a < MT; ++a)
 #pragma unroll
