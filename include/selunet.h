@@ -310,6 +310,14 @@ int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, doubl
  * selunet_bn_stats_finalize (model.py:12 BatchNorm2d batch statistics), numerically two-pass. */
 int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab,
                                  int32_t dtype, void* stream);
+/* Adaptive second pass: uvar[c] = the first pass's unbiased variance (selunet_bn_stats_finalize with
+ * running_var = a zeroed scratch, running_mean = NULL, momentum 1). A group of 4 channels is re-read
+ * (as selunet_bn_centered_partials) only if one of them has center^2 > ratio * uvar — where
+ * E[y^2] - mean^2 loses digits; the others write the sums that make the centered finalize return
+ * the first pass's variance. Same slab layout and finalize. */
+int selunet_bn_centered_partials_adaptive(const void* y, int64_t m, int32_t c, const float* center,
+                                          const float* uvar, float ratio, float* slab, int32_t dtype,
+                                          void* stream);
 int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums,
                                        int64_t count, int32_t c, const float* center,
                                        const float* conv_bias, const float* gamma, const float* beta,

@@ -46,6 +46,23 @@ def read_patch(data_dir, input_file, label_file, patch_mag=200, patch_size=256):
     return inp.astype(np.float32), lab.astype(np.uint8), input_file.split("_input")[0]
 
 
+HED_FROM_RGB_H = (1.8779827368521353, -0.06590806222356332, -0.6019073634392891)  # inv(rgb_from_hed)[:, 0]
+
+
+def rgb2gh(rgb):
+    """RGB2GH (utils/data_utils.py:13-27) restated without cv2/skimage: cv2.cvtColor(RGB2GRAY) of a
+    float32 image = 0.299 R + 0.587 G + 0.114 B; skimage.color.separate_stains(rgb, hed_from_rgb)
+    (skimage >= 0.19 form) = (log(max(rgb, 1e-6)) / log(1e-6)) @ hed_from_rgb, clamped at 0, column
+    0; min-max normalised with the reference's constants. Parity unpinned (neither library is
+    importable here, and the skimage form is version-dependent)."""
+    r, g, b = rgb[..., 0], rgb[..., 1], rgb[..., 2]
+    gray = r * np.float32(0.299) + g * np.float32(0.587) + b * np.float32(0.114)
+    q = np.log(np.maximum(rgb, np.float32(1e-6))) / np.float32(np.log(np.float32(1e-6)))
+    st = np.maximum(q.astype(np.float64) @ np.array(HED_FROM_RGB_H), 0.0)
+    h = (st - (-0.66781543)) / (1.87798274 - (-0.66781543))
+    return np.concatenate((gray[..., None], h[..., None]), axis=-1).astype(np.float32)
+
+
 def transform(inp, lab, flips=0, train=True):
     """Normalization -> [RandomFlip] -> ToTensor (train.py:355-356) -> (x float32 [3,H,W],
     label float32 [H,W] as train.py:189-191 hands it to BCEWithLogitsLoss)."""
@@ -88,12 +105,14 @@ def construct_test(data_dir, test_fold=1):
     return np.vstack([tum, non])
 
 
-def batch(data_dir, pairs, flips=None, train=True, patch_mag=200, patch_size=256):
+def batch(data_dir, pairs, flips=None, train=True, patch_mag=200, patch_size=256, input_type="RGB"):
     """DataLoader's default collate of __getitem__ + transform over `pairs` (train.py:378-381)
     -> (x float32 [N,3,H,W], label float32 [N,H,W], ids)."""
     xs, ls, ids = [], [], []
     for i, (a, b) in enumerate(pairs):
         inp, lab, pid = read_patch(data_dir, str(a), str(b), patch_mag, patch_size)
+        if input_type == "GH":
+            inp = rgb2gh(inp)
         x, t = transform(inp, lab, 0 if flips is None else int(flips[i]), train)
         xs.append(x)
         ls.append(t)

@@ -116,6 +116,7 @@ SIGNATURES = {
     "selunet_bn_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, c_float, c_float,
                                             P, P, P, P, P]),
     "selunet_bn_centered_partials": (c_int32, [P, c_int64, c_int32, P, P, c_int32, P]),
+    "selunet_bn_centered_partials_adaptive": (c_int32, [P, c_int64, c_int32, P, P, c_float, P, c_int32, P]),
     "selunet_bn_stats_finalize_centered": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P,
                                                      c_float, c_float, P, P, P, P, P]),
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),

@@ -230,6 +230,10 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
           bh[b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
           bl[b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
         }
+#if (SELUNET_GABL & 2)
+        asm volatile("" :: "v"(ah[0]), "v"(al[MT - 1]), "v"(bh[0]), "v"(bl[NT - 1]));
+        continue;
+#endif
 #pragma unroll
         for (int a = 0; a < MT; ++a)
 #pragma unroll

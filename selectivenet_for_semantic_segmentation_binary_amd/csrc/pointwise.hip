@@ -308,17 +308,33 @@ __global__ void channel_sum_kernel(const T* __restrict__ x, int64_t m, int C, fl
 // (center = the first pass's mean) -> slab [rows][2][C]. E[y^2] - mean^2 from the conv epilogue's
 // sums loses ~eps * mean^2 / var of the variance (the first layer's invstd came out 14x further from
 // the fp64 value than the reference's); the centered sums do not.
+//
+// Adaptive form (uvar != NULL, selunet_bn_centered_partials_adaptive): uvar = the first pass's
+// unbiased variance n/(n-1) * (E[y^2] - mean^2). The first pass loses ~eps * (1 + mean^2/var) of
+// the variance, so a group of 4 channels is re-read only if one of them has mean^2 > ratio * var;
+// the others emit the sums that reproduce the first pass's variance exactly in the centered
+// finalize (sum d = 0, sum d^2 = (n-1) * uvar, in slab row 0) — same outputs, no pass over y.
 template <typename T>
 __global__ void bn_centered_partials_kernel(const T* __restrict__ y, int64_t m, int C, const float* __restrict__ center,
-                                            float* slab) {
+                                            const float* __restrict__ uvar, float ratio, float* slab) {
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   const int c0 = (threadIdx.x % (C >> 2)) * 4;
   const f32x4 mu = *reinterpret_cast<const f32x4*>(center + c0);
-  channel_loop<T>(m, C, [&](int64_t p, int c) {
-    const f32x4 d = Vec4<T>::load(y + p * C + c) - mu;
-    acc[0] += d;
-    acc[1] += d * d;
-  });
+  bool need = true;
+  if (uvar) {
+    const f32x4 uv = *reinterpret_cast<const f32x4*>(uvar + c0);
+    need = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) need |= !(mu[e] * mu[e] <= ratio * uv[e]);  // NaN / tiny var: re-read
+    if (!need && blockIdx.x == 0 && threadIdx.x < (C >> 2)) acc[1] = uv * (float)(m - 1);
+  }
+  if (need) {
+    channel_loop<T>(m, C, [&](int64_t p, int c) {
+      const f32x4 d = Vec4<T>::load(y + p * C + c) - mu;
+      acc[0] += d;
+      acc[1] += d * d;
+    });
+  }
   channel_block_reduce<2>(acc, C, slab + (int64_t)blockIdx.x * 2 * C);
 }
 
@@ -1449,8 +1465,17 @@ int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const floa
                                  void* stream) {
   SELUNET_REQUIRE(y && center && slab && m > 0 && ok_channels(c), "bn_centered_partials: bad arguments (C=%d)", c);
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB),
-                                       0, as_stream(stream), (const T*)y, m, c, center, slab));
+                                       0, as_stream(stream), (const T*)y, m, c, center, nullptr, 0.0f, slab));
   return check_launch("bn_centered_partials");
+}
+
+int selunet_bn_centered_partials_adaptive(const void* y, int64_t m, int32_t c, const float* center, const float* uvar,
+                                          float ratio, float* slab, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && center && uvar && slab && m > 1 && ok_channels(c) && ratio >= 0.0f,
+                  "bn_centered_partials_adaptive: bad arguments (C=%d)", c);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB),
+                                       0, as_stream(stream), (const T*)y, m, c, center, uvar, ratio, slab));
+  return check_launch("bn_centered_partials_adaptive");
 }
 
 int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,

@@ -22,6 +22,15 @@ constexpr int IO_TPB = 256;
 // One thread per (image, row, 4-pixel group): reads 12 B of RGB + 4 B of label (the whole
 // 4-pixel group), writes 3 x 16 B of NCHW planes + 16 B of target. Flips are applied on the
 // READ side (output pixel (y, x) reads source (y', x')), so the stores stay contiguous.
+// CIN = 2: input_type 'GH' (utils/data_utils.py:13-27, applied before Normalization at :223-224):
+// channel 0 = cv2 RGB2GRAY of the [0,1] fp32 image (0.299 R + 0.587 G + 0.114 B), channel 1 = the
+// hematoxylin stain of skimage.color.separate_stains(rgb, hed_from_rgb) (stains = (log(max(rgb,
+// 1e-6)) / log(1e-6)) @ hed_from_rgb, clamped at 0; column 0 of inv(rgb_from_hed)) min-max
+// normalised with the reference's constants -0.66781543 / 1.87798274.
+constexpr double HED_H0 = 1.8779827368521353, HED_H1 = -0.06590806222356332, HED_H2 = -0.6019073634392891;
+constexpr double GH_HMIN = -0.66781543, GH_HMAX = 1.87798274;
+
+template <int CIN>
 __global__ void prep_batch_kernel(const uint8_t* __restrict__ img, const uint8_t* __restrict__ lab,
                                   const uint8_t* __restrict__ flips, int n, int h, int w, float* __restrict__ x,
                                   float* __restrict__ target) {
@@ -35,19 +44,31 @@ __global__ void prep_batch_kernel(const uint8_t* __restrict__ img, const uint8_t
     const int f = flips ? flips[b] : 0;
     const int ys = (f & 2) ? h - 1 - y : y;  // np.flipud (utils/data_utils.py:118-121)
     const int64_t src_row = ((int64_t)b * h + ys) * w;
-    float xv[3][4];
+    float xv[CIN][4];
     float tv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int xo = xq * 4 + j;
       const int xs = (f & 1) ? w - 1 - xo : xo;  // np.fliplr (utils/data_utils.py:113-116)
       const uint8_t* p = img + (src_row + xs) * 3;
+      // input/255.0 in float64, astype(float32) (utils/data_utils.py:220-221)
+      float v[3];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        // input/255.0 in float64, astype(float32) (utils/data_utils.py:220-221), then
+      for (int c = 0; c < 3; ++c) v[c] = (float)((double)p[c] / 255.0);
+      if constexpr (CIN == 3) {
         // (x - 0.5) / 0.5 in float32 (Normalization, utils/data_utils.py:101)
-        const float v = (float)((double)p[c] / 255.0);
-        xv[c][j] = (v - 0.5f) / 0.5f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) xv[c][j] = (v[c] - 0.5f) / 0.5f;
+      } else {
+        const float gray = v[0] * 0.299f + v[1] * 0.587f + v[2] * 0.114f;
+        const float la = logf(1e-6f);
+        double st = 0.0;
+        st += (double)(logf(fmaxf(v[0], 1e-6f)) / la) * HED_H0;
+        st += (double)(logf(fmaxf(v[1], 1e-6f)) / la) * HED_H1;
+        st += (double)(logf(fmaxf(v[2], 1e-6f)) / la) * HED_H2;
+        const float hn = (float)((fmax(st, 0.0) - GH_HMIN) / (GH_HMAX - GH_HMIN));
+        xv[0][j] = (gray - 0.5f) / 0.5f;
+        xv[1][j] = (hn - 0.5f) / 0.5f;
       }
       // (label/255.0).astype(uint8): truncation, so only 255 -> 1
       tv[j] = (float)(uint8_t)((double)lab[src_row + xs] / 255.0);
@@ -55,8 +76,8 @@ __global__ void prep_batch_kernel(const uint8_t* __restrict__ img, const uint8_t
     const int64_t plane = (int64_t)h * w;
     const int64_t o = (int64_t)y * w + xq * 4;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-      *reinterpret_cast<f32x4*>(x + ((int64_t)b * 3 + c) * plane + o) = f32x4{xv[c][0], xv[c][1], xv[c][2], xv[c][3]};
+    for (int c = 0; c < CIN; ++c)
+      *reinterpret_cast<f32x4*>(x + ((int64_t)b * CIN + c) * plane + o) = f32x4{xv[c][0], xv[c][1], xv[c][2], xv[c][3]};
     *reinterpret_cast<f32x4*>(target + (int64_t)b * plane + o) = f32x4{tv[0], tv[1], tv[2], tv[3]};
   }
 }
@@ -115,13 +136,13 @@ extern "C" {
 int selunet_prep_batch(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n, int32_t h, int32_t w,
                        int32_t cin, float* x, float* target, void* stream) {
   SELUNET_REQUIRE(img && lab && x && target && n > 0 && h > 0 && w > 0, "prep_batch: bad arguments");
-  SELUNET_REQUIRE(cin == 3, "prep_batch: RGB patches only (input_type 'RGB', utils/data_utils.py:223-226)");
+  SELUNET_REQUIRE(cin == 3 || cin == 2, "prep_batch: cin 3 (input_type 'RGB') or 2 ('GH', utils/data_utils.py:223-224)");
   SELUNET_REQUIRE(w % 4 == 0, "prep_batch: width must be a multiple of 4");
   SELUNET_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)target & 15) == 0, "prep_batch: outputs must be 16-B aligned");
   const int64_t total = (int64_t)n * h * (w / 4);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(total, IO_TPB), 8192));
-  hipLaunchKernelGGL(prep_batch_kernel, dim3(grid), dim3(IO_TPB), 0, as_stream(stream), img, lab, flips, n, h, w, x,
-                     target);
+  hipLaunchKernelGGL(cin == 3 ? prep_batch_kernel<3> : prep_batch_kernel<2>, dim3(grid), dim3(IO_TPB), 0,
+                     as_stream(stream), img, lab, flips, n, h, w, x, target);
   return check_launch("prep_batch");
 }
 

@@ -131,13 +131,21 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
 
 
 # ----------------------------------------------------------------------------- GPU batches
-def prep_batch(images_u8: torch.Tensor, labels_u8: torch.Tensor, flips: torch.Tensor | None = None):
-    """uint8 NHWC patches + uint8 masks on the GPU -> (x fp32 [N,3,H,W], target fp32 [N,H,W]),
-    the reference's Normalization + RandomFlip + ToTensor + label/255 truncation."""
+_CIN = {"RGB": 3, "GH": 2}
+
+
+def prep_batch(images_u8: torch.Tensor, labels_u8: torch.Tensor, flips: torch.Tensor | None = None,
+               input_type: str = "RGB"):
+    """uint8 NHWC patches + uint8 masks on the GPU -> (x fp32 [N,C,H,W], target fp32 [N,H,W]),
+    the reference's [RGB2GH +] Normalization + RandomFlip + ToTensor + label/255 truncation
+    (C = 3 for input_type 'RGB', 2 for 'GH': utils/data_utils.py:13-27, 223-224)."""
+    if input_type not in _CIN:
+        raise NotImplementedError(f"input_type {input_type!r}: 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
     for name, t in (("images", images_u8), ("labels", labels_u8), ("flips", flips)):
         if t is not None and (t.device.type != "cuda" or t.dtype != torch.uint8 or not t.is_contiguous()):
             raise RuntimeError(f"prep_batch: {name} must be a contiguous cuda uint8 tensor")
-    n, h, w, c = images_u8.shape
+    n, h, w, _ = images_u8.shape
+    c = _CIN[input_type]
     if labels_u8.shape != (n, h, w) or (flips is not None and flips.shape != (n,)):
         raise ValueError("prep_batch: labels must be [N,H,W] and flips [N]")
     x = torch.empty(n, c, h, w, dtype=torch.float32, device=images_u8.device)
@@ -158,8 +166,9 @@ class BatchLoader:
     """
 
     def __init__(self, ds: PatchSet, batch_size: int, shuffle: bool, random_flip: bool, device, seed: int = 0,
-                 max_batches: int = 0):
+                 max_batches: int = 0, input_type: str = "RGB"):
         self.ds, self.bs, self.shuffle, self.flip = ds, int(batch_size), shuffle, random_flip
+        self.input_type = input_type
         self.device, self.seed, self.max_batches = device, seed, max_batches
         self.epoch = 0
         self.dropped = 0
@@ -213,5 +222,5 @@ class BatchLoader:
             lb = lb.to(self.device, non_blocking=True)
             fl = fl.to(self.device, non_blocking=True)
             parallel.set_global_batch(gb)
-            x, t = prep_batch(im, lb, fl)
+            x, t = prep_batch(im, lb, fl, self.input_type)
             yield x, t

@@ -25,6 +25,9 @@ from . import layout as LY
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+# fp32 BatchNorm statistics: channel groups with mean^2 > BN_CENTER_RATIO x the one-pass variance get
+# the centered second pass over y (selunet_bn_centered_partials_adaptive); None: every channel does
+BN_CENTER_RATIO = None if os.environ.get("SELUNET_BN_TWOPASS", "0") == "1" else 1.0
 FIRST_KPAD = 32  # packed K of encoder_layer_1_1 (9 * C_in <= 27), see selunet_first_conv_fwd
 
 
@@ -309,14 +312,22 @@ class Engine:
             # fp32 (parity): two-pass statistics — the epilogue's sums give the batch mean, a second
             # pass over y sums (y - mean) and (y - mean)^2 for the variance, then the finalize with the
             # running-statistic updates (selunet_bn_centered_partials)
+            # (adaptive: only channel groups whose mean^2 exceeds BN_CENTER_RATIO x the one-pass variance
+            # are re-read — where E[y^2] - mean^2 loses digits; SELUNET_BN_TWOPASS=1 re-reads all)
             ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
+            uvar = K.keep(torch.zeros(co, dtype=torch.float32, device=dev)) if BN_CENTER_RATIO is not None else None
             K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
                    K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
-                   None, None, None, BN_MOMENTUM, BN_EPS, K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift),
-                   self.stream)
+                   None, K.ptr(uvar), None, 1.0 if uvar is not None else BN_MOMENTUM, BN_EPS, K.ptr(mean),
+                   K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
             rows2 = K.query("selunet_channel_slab_rows", M)
             slab2 = K.keep(torch.empty(rows2, 2, co, dtype=torch.float32, device=dev))
-            K.call("selunet_bn_centered_partials", K.ptr(y), M, co, K.ptr(mean), K.ptr(slab2), self.code, self.stream)
+            if uvar is not None:
+                K.call("selunet_bn_centered_partials_adaptive", K.ptr(y), M, co, K.ptr(mean), K.ptr(uvar),
+                       BN_CENTER_RATIO, K.ptr(slab2), self.code, self.stream)
+            else:
+                K.call("selunet_bn_centered_partials", K.ptr(y), M, co, K.ptr(mean), K.ptr(slab2), self.code,
+                       self.stream)
             K.call("selunet_bn_stats_finalize_centered", K.ptr(slab2), rows2, K.ptr(ws), None, M, co, K.ptr(mean),
                    K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
                    K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),

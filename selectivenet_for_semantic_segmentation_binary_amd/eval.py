@@ -72,8 +72,8 @@ def evaluate(args):
     from . import metrics as MT
     from . import net_utils
 
-    if args.input_type != 'RGB':
-        raise NotImplementedError("input_type 'RGB' only (GH / H_RGB need cv2 / skimage colour transforms)")
+    if args.input_type not in ('RGB', 'GH'):
+        raise NotImplementedError("input_type 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
     device = torch.device("cuda", args.local_rank[0])
     torch.cuda.set_device(device)
     dt = torch.bfloat16 if args.compute_dtype == 'bf16' else torch.float32
@@ -92,7 +92,8 @@ def evaluate(args):
         raise NotImplementedError("ensembles of selective networks are not supported (eval.py:185, '선택 불가')")
 
     ds = load_test_set(args)
-    loader = D.BatchLoader(ds, args.batch_size, shuffle=False, random_flip=False, device=device)
+    loader = D.BatchLoader(ds, args.batch_size, shuffle=False, random_flip=False, device=device,
+                           input_type=args.input_type)
     ev = MT.SegMetrics(device, selective=bool(args.select_eval), rule="eval", cut_off=args.cut_off,
                        s_cut_off=args.s_cut_off, output_scale=args.single_scale)
     print("Model Prediction...")

@@ -22,7 +22,7 @@ What differs, by design:
   * Data: `--data_dir synthetic[:N]` uses the seeded synthetic patches; any other
     directory is read through the reference's split files ({k}-fold_{,non_}tumorable_data.npy) and
     decoded once into uint8 caches (`data.decode_patch_list`); normalisation and flips run on the
-    GPU. input_type 'RGB'; model_arch 'UNet_B' with loss 'BCElogit', or the CE `UNet`
+    GPU. input_type 'RGB' or 'GH'; model_arch 'UNet_B' with loss 'BCElogit', or the CE `UNet`
     (model_arch 'UNet', loss 'CE', n_cls 2: CrossEntropyLoss aux + calc_selective_risk_image, argmax
     masks as train.py:207-219).
   * TensorBoard scalars are written when torch.utils.tensorboard is importable, otherwise as JSON
@@ -185,8 +185,8 @@ def train(args, ckpt_dir, log_dir):
                                   "with 'CE' (train.py:71-86 allows the mixed pairs; they are not implemented)")
     if ce and args.n_cls != 2:
         raise NotImplementedError("the CE UNet's on-device metrics are binary: n_cls 2 (train.py:23 default)")
-    if args.input_type != 'RGB':
-        raise NotImplementedError("input_type 'RGB' only (GH / H_RGB need cv2 / skimage colour transforms)")
+    if args.input_type not in ('RGB', 'GH'):
+        raise NotImplementedError("input_type 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gpu = int(os.environ.get("SELUNET_GPU_ID", args.local_rank[0]))
@@ -232,9 +232,9 @@ def train(args, ckpt_dir, log_dir):
 
     ds_train, ds_val = load_data(args, args.seed)
     loader_train = D.BatchLoader(ds_train, args.batch_size, shuffle=True, random_flip=True, device=device,
-                                 seed=args.seed, max_batches=args.steps_per_epoch)
+                                 seed=args.seed, max_batches=args.steps_per_epoch, input_type=args.input_type)
     loader_val = D.BatchLoader(ds_val, args.batch_size, shuffle=False, random_flip=False, device=device,
-                               seed=args.seed, max_batches=args.val_steps)
+                               seed=args.seed, max_batches=args.val_steps, input_type=args.input_type)
     log(f'# of gpu: {world}, gpu id: {args.local_rank}\n')
 
     writer_train = _Scalars(os.path.join(log_dir, 'train'), rank == 0)

@@ -32,3 +32,21 @@ def test_loader_batches_match_reference_dataset(tmp_path, train):
         assert x.dtype == torch.float32 and tuple(x.shape) == xe.shape
         assert np.array_equal(x.cpu().numpy(), xe) and np.array_equal(t.cpu().numpy(), te)
     assert (flipped > 0) == train
+
+
+def test_gh_batches_match_restatement(tmp_path):
+    """input_type 'GH' (utils/data_utils.py:13-27, 223-224) on the GPU vs the oracle's RGB2GH
+    restatement: gray bit-exact up to the fused multiply-add of the three-term sum (1e-6), the
+    hematoxylin channel within 1e-5 (logf vs numpy's log). Parity unpinned against the reference's
+    cv2/skimage (absent here)."""
+    root = make_patch_dir(str(tmp_path), per_fold=4, size=32)
+    tr, _ = D.construct_train_valid(root, test_fold=2)
+    ds = D.decode_patch_list(root, tr, patch_mag=200, patch_size=32, cache=False)
+    loader = D.BatchLoader(ds, batch_size=4, shuffle=True, random_flip=True, device="cuda", seed=3, input_type="GH")
+    for (gb, idx, fl), (x, t) in zip(loader._plan(), loader):
+        xe, te, _ = OD.batch(root, tr[idx], flips=fl, train=True, patch_mag=200, patch_size=32, input_type="GH")
+        assert tuple(x.shape) == xe.shape and xe.shape[1] == 2
+        xg = x.cpu().numpy()
+        assert np.abs(xg[:, 0] - xe[:, 0]).max() <= 1e-6
+        assert np.abs(xg[:, 1] - xe[:, 1]).max() <= 1e-5
+        assert np.array_equal(t.cpu().numpy(), te)

@@ -1,7 +1,7 @@
 """Time the ConvTranspose2d GEMMs (selunet_gemm_gather SCATTER2X forward, taps=4 dgrad) at the
-bench shapes (bs=128, bf16) — profiling tool, like tools/conv_bench.py.
+bench shapes (bs=128, bf16; --x2: the fp32 split-fp16 kernels) — profiling tool, like tools/conv_bench.py.
 
-    python tools/convt_bench.py [--batch 128] [--iters 10]
+    python tools/convt_bench.py [--batch 128] [--iters 10] [--x2]
 """
 import argparse
 import os
@@ -32,31 +32,44 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--x2", action="store_true")
     a = ap.parse_args()
-    n, dt, dev = a.batch, torch.bfloat16, "cuda"
+    n, dev = a.batch, "cuda"
+    dt = torch.float32 if a.x2 else torch.bfloat16
+    amax = torch.full((1,), 8.0, device=dev)
     tot = 0.0
     for name, ci, co, r in UPS:
         x = torch.randn(n * r * r, ci, device=dev).to(dt)
         sc, sh = torch.rand(ci, device=dev) + 0.5, torch.randn(ci, device=dev) * 0.1
-        w = (torch.randn(4 * co, ci, device=dev) * 0.05).to(dt)
+        w = (torch.randn(4 * co * ci + 4 * co, device=dev).abs() * 1e-3 + 1e-3) if a.x2 else \
+            (torch.randn(4 * co, ci, device=dev) * 0.05).to(dt)
         bias = torch.randn(co, device=dev)
         out = torch.empty(n * 4 * r * r, co, device=dev, dtype=dt)
         g = K.gather(n, r, r, 1, K.source(x, ci, sc, sh))
         ep = K.Epilogue(K.ptr(out), None, K.ptr(bias), None, K.EP_SCATTER2X, 0)
-        f = lambda: K.call("selunet_gemm_gather", g, K.ptr(w), 4 * co, ci, ep, K.BF16, K.stream_ptr())  # noqa: E731
+        if a.x2:
+            f = lambda: K.call("selunet_gemm_gather_x2", g, K.ptr(w), 4 * co, ci, ep, K.ptr(amax), None,  # noqa: E731
+                               K.stream_ptr())
+        else:
+            f = lambda: K.call("selunet_gemm_gather", g, K.ptr(w), 4 * co, ci, ep, K.BF16, K.stream_ptr())  # noqa: E731
         ms = timed(f, a.iters)
-        byt = (x.numel() + out.numel()) * 2
+        byt = (x.numel() + out.numel()) * x.element_size()
         tot += ms
         print(f"fwd   {name} {ci}->{co} @{r}: {ms:.3f} ms  {2 * n * r * r * ci * 4 * co / ms / 1e9:7.1f} TF/s "
               f"{byt / ms / 1e6:7.1f} GB/s", flush=True)
         du = torch.randn(n * 4 * r * r, co, device=dev).to(dt)
-        wd = (torch.randn(ci, 4 * co, device=dev) * 0.05).to(dt)
+        wd = (torch.randn(ci * 4 * co + ci, device=dev).abs() * 1e-3 + 1e-3) if a.x2 else \
+            (torch.randn(ci, 4 * co, device=dev) * 0.05).to(dt)
         dz = torch.empty(n * r * r, ci, device=dev, dtype=dt)
         gd = K.gather(n, r, r, 4, K.source(du, co))
         epd = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
-        fd = lambda: K.call("selunet_gemm_gather", gd, K.ptr(wd), ci, 4 * co, epd, K.BF16, K.stream_ptr())  # noqa: E731
+        if a.x2:
+            fd = lambda: K.call("selunet_gemm_gather_x2", gd, K.ptr(wd), ci, 4 * co, epd, K.ptr(amax), None,  # noqa: E731
+                                K.stream_ptr())
+        else:
+            fd = lambda: K.call("selunet_gemm_gather", gd, K.ptr(wd), ci, 4 * co, epd, K.BF16, K.stream_ptr())  # noqa: E731
         ms = timed(fd, a.iters)
-        byt = (du.numel() + dz.numel()) * 2
+        byt = (du.numel() + dz.numel()) * du.element_size()
         tot += ms
         print(f"dgrad {name} {co}->{ci} @{r}: {ms:.3f} ms  {2 * n * r * r * ci * 4 * co / ms / 1e9:7.1f} TF/s "
               f"{byt / ms / 1e6:7.1f} GB/s", flush=True)
