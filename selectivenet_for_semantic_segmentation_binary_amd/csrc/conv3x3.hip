@@ -22,6 +22,11 @@
 #ifndef SELUNET_ABL
 #define SELUNET_ABL 0
 #endif
+// SELUNET_X2MFO: split-fp16 MFMA issue order (0: the three products of one accumulator back to back,
+// 1: product-major over the wave's accumulators) — A/B switch
+#ifndef SELUNET_X2MFO
+#define SELUNET_X2MFO 0
+#endif
 
 namespace selunet {
 
@@ -473,6 +478,21 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
         asm volatile("" :: "v"(ah[0]), "v"(al[MT - 1]), "v"(bh[0]), "v"(bl[NT - 1]));
         continue;
 #endif
+#if SELUNET_X2MFO
+        // product-major order: MT * NT independent accumulators between two MFMAs of one chain
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+#else
 #pragma unroll
         for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -481,6 +501,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
           }
+#endif
       }
       return;
     }

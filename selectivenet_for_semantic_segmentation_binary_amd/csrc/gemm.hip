@@ -1193,7 +1193,10 @@ extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, i
   SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
                   "gemm_gather_x2: every source needs its range word (amax0, amax1)");
   hipStream_t st = as_stream(stream);
-  const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
+#ifndef SELUNET_X2_BN64
+#define SELUNET_X2_BN64 0
+#endif
+  const bool bn128 = !SELUNET_X2_BN64 && n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
   const int64_t P = gather_rows(g, n_cols);
   const float* wcs = w + (int64_t)n_cols * k_pad;
   if (bn128)
