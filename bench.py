@@ -419,10 +419,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # (rehearsal of the N > 1 path on a one-GPU box: SELUNET_BENCH_ONE_DEVICE=1 puts every rank on
+    # cuda:0 and uses gloo, which RCCL cannot; the driver's multi-GPU runs use one GPU per rank, RCCL)
+    one_dev = os.environ.get("SELUNET_BENCH_ONE_DEVICE", "0") == "1"
+    if one_dev:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        parallel.init_data_parallel(backend="nccl")
+        parallel.init_data_parallel(backend="gloo" if one_dev else "nccl")
         # the per-kernel event records add host work to the small per-GPU steps of the scaling runs
         args.no_kernel_timing = True
 
