@@ -171,19 +171,38 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
   const bool fw = r < fwd_rows;
   const int row = fw ? r : r - fwd_rows;
   const int len = ct ? (fw ? ci : 4 * co) : (fw ? 9 * ci : 9 * co);
-  const int rk = fw ? ci : co;  // conv3x3: k = tap * rk + channel
   const float* w = d.w;
-  auto val = [&](int k) -> float {
-    if (ct) {  // fwd row (ab, o) = ab * co + o, k = c; dgrad row c, k = ab * co + o
-      const int ab = fw ? row / co : k / co, o = fw ? row - ab * co : k - (k / co) * co, c = fw ? k : row;
-      return w[((int64_t)c * co + o) * 4 + ab];
-    }
-    const int tap = k / rk, c = k - tap * rk;
-    return fw ? w[((int64_t)row * ci + c) * 9 + tap] : w[((int64_t)c * ci + row) * 9 + (8 - tap)];
-  };
-  float m = 0.0f;
-  for (int k = threadIdx.x; k < len; k += 256) m = fmaxf(m, fabsf(val(k)));
+  // the row is gathered in SOURCE order (j walks the fp32 master's memory, contiguous runs of 9 taps
+  // / 4 positions) into LDS at its packed position k, then max-reduced and written in k order
+  __shared__ float rowv[9 * 512];
   __shared__ float red[256];
+  float m = 0.0f;
+  for (int j = threadIdx.x; j < len; j += 256) {
+    int k;
+    int64_t src;
+    if (ct) {
+      if (fw) {  // row (ab, o) = ab * co + o, k = c: w[c][o][ab] (stride 4 co)
+        const int ab = row / co, o = row - ab * co;
+        k = j;
+        src = ((int64_t)j * co + o) * 4 + ab;
+      } else {   // row c, k = ab * co + o: w[c][o][ab] contiguous over j = o * 4 + ab
+        const int o = j >> 2, ab = j & 3;
+        k = ab * co + o;
+        src = (int64_t)row * 4 * co + j;
+      }
+    } else if (fw) {  // row o, k = tap * ci + c: w[o][c][tap] contiguous over j = c * 9 + tap
+      const int c = j / 9, tap = j - c * 9;
+      k = tap * ci + c;
+      src = (int64_t)row * 9 * ci + j;
+    } else {  // row c, k = tap * co + o (taps flipped): w[o][c][8 - tap], runs of 9 over j = o * 9 + tp
+      const int o = j / 9, tp = j - o * 9;
+      k = (8 - tp) * co + o;
+      src = ((int64_t)o * ci + row) * 9 + tp;
+    }
+    const float v = w[src];
+    rowv[k] = v;
+    m = fmaxf(m, fabsf(v));
+  }
   red[threadIdx.x] = m;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -196,7 +215,7 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
   const float sc = x2_scale(red[0], &unscale);
   _Float16* out = reinterpret_cast<_Float16*>(base + (int64_t)row * len);
   for (int k = threadIdx.x; k < len; k += 256) {
-    const float v = val(k) * sc;
+    const float v = rowv[k] * sc;
     const _Float16 h = (_Float16)v;
     const _Float16 lo = (_Float16)(v - (float)h);
     const int grp = k >> 5, j = k & 31;
@@ -1299,6 +1318,8 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
                           d.co % 32 == 0,
                       "pack_weights: split-fp16 entry %d needs fp32, fwd, k_pad = %s and ci, co multiples of 32", t,
                       ct ? "ci" : "9*ci");
+      SELUNET_REQUIRE(ct ? (d.ci <= 4608 && 4 * d.co <= 4608) : (d.ci <= 512 && d.co <= 512),
+                      "pack_weights: split-fp16 entry %d: a packed row is staged in LDS (<= 4608 values)", t);
       lx.d[lx.n] = d;
       lx.d[lx.n].offset = xrows;
       ++lx.n;
