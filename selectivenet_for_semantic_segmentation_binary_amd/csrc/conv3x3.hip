@@ -27,6 +27,9 @@
 #ifndef SELUNET_X2MFO
 #define SELUNET_X2MFO 0
 #endif
+#ifndef SELUNET_X2HOIST
+#define SELUNET_X2HOIST 0
+#endif
 
 namespace selunet {
 
@@ -449,6 +452,37 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
     if constexpr (X2) {
+#if SELUNET_X2HOIST
+      // both k-steps' fragments read before the first MFMA (A/B experiment)
+      f16x8 fa[2][MT], fl[2][MT], gh[2][NT], gl[2][NT];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          const unsigned char* p = a_src + (hrow0[a] + tap_off) * AROWB + ((hsw0[a] ^ dy) & 1) * 16;
+          fa[ks][a] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          fl[ks][a] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          const unsigned char* p = b_src + (wn * 64 + b * 32 + l32) * ROWB + half * 16;
+          gh[ks][b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
+          gl[ks][b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[ks][a], gl[ks][b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[ks][a], gh[ks][b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[ks][a], gh[ks][b], acc[a][b], 0, 0, 0);
+          }
+      return;
+#endif
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         f16x8 ah[MT], al[MT], bh[NT], bl[NT];
