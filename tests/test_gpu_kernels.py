@@ -734,3 +734,51 @@ def test_conv3x3_bf16_persist_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
         check_bnb_sums(slab.cpu(), dx.float().cpu(), yprev.float().cpu(), sc.cpu(), sh.cpu(), mean.cpu(),
                        invstd.cpu(), tol=1e-4)
     assert rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("c", [64, 256])
+def test_bn_adaptive_centered_variance(c):
+    """selunet_bn_centered_partials_adaptive (fp32 BatchNorm variance, engine default): channels
+    whose mean^2 exceeds ratio x the one-pass variance are re-read (centered sums), the others reuse
+    the one-pass variance exactly. Against the fp64 batch statistics of y: mean within 1e-6 of the
+    scale, variance within 1e-5 relative on the re-read groups (where the one-pass E[y^2] - mean^2
+    is off by ~eps * mean^2 / var) and within 1e-5 on the others; running statistics updated once."""
+    M = 50000
+    g = torch.Generator().manual_seed(11)
+    means = torch.where(torch.arange(c) % 8 < 4, 300.0, 0.3)  # groups of 4: large / small mean^2 / var
+    y = (torch.randn(M, c, generator=g) + means).float().to(DEV)
+    rows = K.query("selunet_channel_slab_rows", M)
+    slab1 = torch.zeros(1, 2, c, device=DEV)
+    slab1[0, 0] = y.double().sum(0).float()          # the conv epilogue's one-pass sums (fp32 slab)
+    slab1[0, 1] = (y.double() ** 2).sum(0).float()
+    ws = torch.empty(K.query("selunet_reduce_ws_bytes", 2 * c) // 8, dtype=torch.float64, device=DEV)
+    gamma, beta = torch.ones(c, device=DEV), torch.zeros(c, device=DEV)
+    outs = []
+    for adaptive in (True, False):
+        mean, invstd, scale, shift = (torch.empty(c, device=DEV) for _ in range(4))
+        uvar = torch.zeros(c, device=DEV)
+        K.call("selunet_bn_stats_finalize", K.ptr(slab1), 1, K.ptr(ws), None, M, c, None, K.ptr(gamma),
+               K.ptr(beta), None, K.ptr(uvar), None, 1.0, 1e-5, K.ptr(mean), K.ptr(invstd), K.ptr(scale),
+               K.ptr(shift), K.stream_ptr())
+        slab2 = torch.empty(rows, 2, c, device=DEV)
+        if adaptive:
+            K.call("selunet_bn_centered_partials_adaptive", K.ptr(y), M, c, K.ptr(mean), K.ptr(uvar), 1.0,
+                   K.ptr(slab2), K.F32, K.stream_ptr())
+        else:
+            K.call("selunet_bn_centered_partials", K.ptr(y), M, c, K.ptr(mean), K.ptr(slab2), K.F32,
+                   K.stream_ptr())
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+        K.call("selunet_bn_stats_finalize_centered", K.ptr(slab2), rows, K.ptr(ws), None, M, c, K.ptr(mean), None,
+               K.ptr(gamma), K.ptr(beta), K.ptr(rm), K.ptr(rv), K.ptr(nbt), 0.1, 1e-5, K.ptr(mean), K.ptr(invstd),
+               K.ptr(scale), K.ptr(shift), K.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((mean.cpu().double(), invstd.cpu().double(), rv.cpu().double(), int(nbt)))
+    yd = y.cpu().double()
+    m64, v64 = yd.mean(0), yd.var(0, unbiased=False)
+    for mean, invstd, rv, nbt in outs:
+        assert nbt == 1
+        assert ((mean - m64).abs() / (m64.abs() + 1)).max() < 1e-6
+        var = 1.0 / invstd ** 2 - 1e-5
+        assert ((var - v64).abs() / v64).max() < 1e-5
+        assert ((rv - (0.9 + 0.1 * v64 * M / (M - 1))).abs()).max() < 1e-5
