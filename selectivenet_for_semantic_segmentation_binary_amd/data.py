@@ -144,7 +144,9 @@ def prep_batch(images_u8: torch.Tensor, labels_u8: torch.Tensor, flips: torch.Te
     for name, t in (("images", images_u8), ("labels", labels_u8), ("flips", flips)):
         if t is not None and (t.device.type != "cuda" or t.dtype != torch.uint8 or not t.is_contiguous()):
             raise RuntimeError(f"prep_batch: {name} must be a contiguous cuda uint8 tensor")
-    n, h, w, _ = images_u8.shape
+    n, h, w, c_img = images_u8.shape
+    if c_img != 3:
+        raise ValueError(f"prep_batch: images must be RGB [N,H,W,3] uint8 (got {tuple(images_u8.shape)})")
     c = _CIN[input_type]
     if labels_u8.shape != (n, h, w) or (flips is not None and flips.shape != (n,)):
         raise ValueError("prep_batch: labels must be [N,H,W] and flips [N]")
