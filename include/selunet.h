@@ -497,9 +497,15 @@ int selunet_adam_step(const selunet_adam_tensor* list, int32_t n, int64_t total_
  * numpy transforms (utils/data_utils.py:94-125,160-168,220-221; train.py:189-191).
  * img: uint8 NHWC [n][h][w][cin] (cin = 3, RGB); lab: uint8 [n][h][w] raw mask values (only 255
  * maps to 1); flips: uint8 [n] (bit 0 = np.fliplr, bit 1 = np.flipud; NULL = none).
- * x: fp32 NCHW [n][3][h][w] = (float32(v/255.0) - 0.5)/0.5; target: fp32 [n][h][w] in {0,1}. */
+ * x: fp32 NCHW [n][3][h][w] = (float32(v/255.0) - 0.5)/0.5; target: fp32 [n][h][w] in {0,1}.
+ * cin = 2: input_type 'GH' (utils/data_utils.py:13-27): x [n][2][h][w] = normalised (cv2 gray,
+ * skimage hematoxylin stain min-max scaled with the reference's constants). */
 int selunet_prep_batch(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n,
                        int32_t h, int32_t w, int32_t cin, float* x, float* target, void* stream);
+/* The same by input_type: mode 0 'RGB', 1 'GH', 2 'H_RGB' (utils/data_utils.py:29-41: the
+ * hematoxylin stain recombined alone by skimage.color.combine_stains; x [n][3][h][w]). */
+int selunet_prep_batch_mode(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n,
+                            int32_t h, int32_t w, int32_t mode, float* x, float* target, void* stream);
 /* Per-batch metrics of train.py:211-238 / eval.py:218-246 accumulated on the device:
  * counts[6] (uint64, caller-zeroed, accumulated across calls) = {cm[0][0], cm[0][1], cm[1][0],
  * cm[1][1], selected, total} with cm[label][pred] = Evaluator.confusion_matrix

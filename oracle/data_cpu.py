@@ -63,6 +63,16 @@ def rgb2gh(rgb):
     return np.concatenate((gray[..., None], h[..., None]), axis=-1).astype(np.float32)
 
 
+def h_rgb(rgb):
+    """H_RGB (utils/data_utils.py:29-41) restated: the hematoxylin stain of separate_stains (as in
+    rgb2gh), recombined alone by skimage.color.combine_stains (>= 0.19 form): rgb =
+    clip(exp(-(stains * -log(1e-6)) @ rgb_from_hed), 0, 1) with stains = (h, 0, 0). Parity unpinned."""
+    q = np.log(np.maximum(rgb, np.float32(1e-6))) / np.float32(np.log(np.float32(1e-6)))
+    h = np.maximum(q.astype(np.float64) @ np.array(HED_FROM_RGB_H), 0.0)
+    out = np.exp(-(h[..., None] * -np.log(1e-6)) * np.array([0.65, 0.70, 0.29]))
+    return np.clip(out, 0, 1).astype(np.float32)
+
+
 def transform(inp, lab, flips=0, train=True):
     """Normalization -> [RandomFlip] -> ToTensor (train.py:355-356) -> (x float32 [3,H,W],
     label float32 [H,W] as train.py:189-191 hands it to BCEWithLogitsLoss)."""
@@ -113,6 +123,8 @@ def batch(data_dir, pairs, flips=None, train=True, patch_mag=200, patch_size=256
         inp, lab, pid = read_patch(data_dir, str(a), str(b), patch_mag, patch_size)
         if input_type == "GH":
             inp = rgb2gh(inp)
+        elif input_type == "H_RGB":
+            inp = h_rgb(inp)
         x, t = transform(inp, lab, 0 if flips is None else int(flips[i]), train)
         xs.append(x)
         ls.append(t)

@@ -162,6 +162,7 @@ SIGNATURES = {
     "selunet_graph_launch": (c_int32, [P, P]),
     "selunet_graph_destroy": (c_int32, [P]),
     "selunet_prep_batch": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
+    "selunet_prep_batch_mode": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
     "selunet_seg_metrics": (c_int32, [P, P, P, c_int64, c_float, c_float, P, P]),
 }
 

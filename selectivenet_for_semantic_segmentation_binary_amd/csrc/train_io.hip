@@ -30,7 +30,11 @@ constexpr int IO_TPB = 256;
 constexpr double HED_H0 = 1.8779827368521353, HED_H1 = -0.06590806222356332, HED_H2 = -0.6019073634392891;
 constexpr double GH_HMIN = -0.66781543, GH_HMAX = 1.87798274;
 
-template <int CIN>
+// HRGB (CIN = 3): input_type 'H_RGB' (utils/data_utils.py:29-41): the hematoxylin stain h of
+// separate_stains as above, recombined alone by skimage.color.combine_stains(stack(h, 0, 0),
+// rgb_from_hed) = clip(exp(-h * (-log 1e-6) * rgb_from_hed[0]), 0, 1), rgb_from_hed[0] =
+// (0.65, 0.70, 0.29).
+template <int CIN, bool HRGB = false>
 __global__ void prep_batch_kernel(const uint8_t* __restrict__ img, const uint8_t* __restrict__ lab,
                                   const uint8_t* __restrict__ flips, int n, int h, int w, float* __restrict__ x,
                                   float* __restrict__ target) {
@@ -55,7 +59,20 @@ __global__ void prep_batch_kernel(const uint8_t* __restrict__ img, const uint8_t
       float v[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) v[c] = (float)((double)p[c] / 255.0);
-      if constexpr (CIN == 3) {
+      if constexpr (HRGB) {
+        const float la = logf(1e-6f);
+        double st = 0.0;
+        st += (double)(logf(fmaxf(v[0], 1e-6f)) / la) * HED_H0;
+        st += (double)(logf(fmaxf(v[1], 1e-6f)) / la) * HED_H1;
+        st += (double)(logf(fmaxf(v[2], 1e-6f)) / la) * HED_H2;
+        const double h = fmax(st, 0.0) * -log(1e-6);
+        const double rf[3] = {0.65, 0.70, 0.29};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float o = (float)fmin(fmax(exp(-h * rf[c]), 0.0), 1.0);
+          xv[c][j] = (o - 0.5f) / 0.5f;
+        }
+      } else if constexpr (CIN == 3) {
         // (x - 0.5) / 0.5 in float32 (Normalization, utils/data_utils.py:101)
 #pragma unroll
         for (int c = 0; c < 3; ++c) xv[c][j] = (v[c] - 0.5f) / 0.5f;
@@ -132,6 +149,19 @@ __global__ void seg_metrics_kernel(const float* __restrict__ out, const float* _
 using namespace selunet;
 
 extern "C" {
+
+int selunet_prep_batch_mode(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n, int32_t h,
+                            int32_t w, int32_t mode, float* x, float* target, void* stream) {
+  SELUNET_REQUIRE(mode >= 0 && mode <= 2, "prep_batch_mode: mode 0 'RGB', 1 'GH', 2 'H_RGB' (got %d)", mode);
+  if (mode != 2) return selunet_prep_batch(img, lab, flips, n, h, w, mode == 0 ? 3 : 2, x, target, stream);
+  SELUNET_REQUIRE(img && lab && x && target && n > 0 && h > 0 && w > 0 && w % 4 == 0, "prep_batch: bad arguments");
+  SELUNET_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)target & 15) == 0, "prep_batch: outputs must be 16-B aligned");
+  const int64_t total = (int64_t)n * h * (w / 4);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(total, IO_TPB), 8192));
+  hipLaunchKernelGGL((prep_batch_kernel<3, true>), dim3(grid), dim3(IO_TPB), 0, as_stream(stream), img, lab, flips, n, h,
+                     w, x, target);
+  return check_launch("prep_batch");
+}
 
 int selunet_prep_batch(const uint8_t* img, const uint8_t* lab, const uint8_t* flips, int32_t n, int32_t h, int32_t w,
                        int32_t cin, float* x, float* target, void* stream) {

@@ -131,16 +131,17 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
 
 
 # ----------------------------------------------------------------------------- GPU batches
-_CIN = {"RGB": 3, "GH": 2}
+_CIN = {"RGB": 3, "GH": 2, "H_RGB": 3}
+_MODE = {"RGB": 0, "GH": 1, "H_RGB": 2}
 
 
 def prep_batch(images_u8: torch.Tensor, labels_u8: torch.Tensor, flips: torch.Tensor | None = None,
                input_type: str = "RGB"):
     """uint8 NHWC patches + uint8 masks on the GPU -> (x fp32 [N,C,H,W], target fp32 [N,H,W]),
     the reference's [RGB2GH +] Normalization + RandomFlip + ToTensor + label/255 truncation
-    (C = 3 for input_type 'RGB', 2 for 'GH': utils/data_utils.py:13-27, 223-224)."""
+    (C = 3 for input_type 'RGB' and 'H_RGB', 2 for 'GH': utils/data_utils.py:13-41, 223-226)."""
     if input_type not in _CIN:
-        raise NotImplementedError(f"input_type {input_type!r}: 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
+        raise ValueError(f"input_type {input_type!r}: 'RGB', 'GH' or 'H_RGB' (utils/data_utils.py:223-226)")
     for name, t in (("images", images_u8), ("labels", labels_u8), ("flips", flips)):
         if t is not None and (t.device.type != "cuda" or t.dtype != torch.uint8 or not t.is_contiguous()):
             raise RuntimeError(f"prep_batch: {name} must be a contiguous cuda uint8 tensor")
@@ -152,8 +153,8 @@ def prep_batch(images_u8: torch.Tensor, labels_u8: torch.Tensor, flips: torch.Te
         raise ValueError("prep_batch: labels must be [N,H,W] and flips [N]")
     x = torch.empty(n, c, h, w, dtype=torch.float32, device=images_u8.device)
     t = torch.empty(n, h, w, dtype=torch.float32, device=images_u8.device)
-    K.call("selunet_prep_batch", K.ptr(images_u8), K.ptr(labels_u8), K.ptr(flips), n, h, w, c, K.ptr(x), K.ptr(t),
-           K.stream_ptr())
+    K.call("selunet_prep_batch_mode", K.ptr(images_u8), K.ptr(labels_u8), K.ptr(flips), n, h, w, _MODE[input_type],
+           K.ptr(x), K.ptr(t), K.stream_ptr())
     return x, t
 
 

@@ -72,8 +72,8 @@ def evaluate(args):
     from . import metrics as MT
     from . import net_utils
 
-    if args.input_type not in ('RGB', 'GH'):
-        raise NotImplementedError("input_type 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
+    if args.input_type not in ('RGB', 'GH', 'H_RGB'):
+        raise ValueError(f"input_type {args.input_type!r}: 'RGB', 'GH' or 'H_RGB' (utils/data_utils.py:223-226)")
     device = torch.device("cuda", args.local_rank[0])
     torch.cuda.set_device(device)
     dt = torch.bfloat16 if args.compute_dtype == 'bf16' else torch.float32

@@ -22,7 +22,7 @@ What differs, by design:
   * Data: `--data_dir synthetic[:N]` uses the seeded synthetic patches; any other
     directory is read through the reference's split files ({k}-fold_{,non_}tumorable_data.npy) and
     decoded once into uint8 caches (`data.decode_patch_list`); normalisation and flips run on the
-    GPU. input_type 'RGB' or 'GH'; model_arch 'UNet_B' with loss 'BCElogit', or the CE `UNet`
+    GPU. input_type 'RGB', 'GH' or 'H_RGB'; model_arch 'UNet_B' with loss 'BCElogit', or the CE `UNet`
     (model_arch 'UNet', loss 'CE', n_cls 2: CrossEntropyLoss aux + calc_selective_risk_image, argmax
     masks as train.py:207-219).
   * TensorBoard scalars are written when torch.utils.tensorboard is importable, otherwise as JSON
@@ -185,8 +185,8 @@ def train(args, ckpt_dir, log_dir):
                                   "with 'CE' (train.py:71-86 allows the mixed pairs; they are not implemented)")
     if ce and args.n_cls != 2:
         raise NotImplementedError("the CE UNet's on-device metrics are binary: n_cls 2 (train.py:23 default)")
-    if args.input_type not in ('RGB', 'GH'):
-        raise NotImplementedError("input_type 'RGB' or 'GH' (H_RGB needs skimage's combine_stains)")
+    if args.input_type not in ('RGB', 'GH', 'H_RGB'):
+        raise ValueError(f"input_type {args.input_type!r}: 'RGB', 'GH' or 'H_RGB' (utils/data_utils.py:223-226)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gpu = int(os.environ.get("SELUNET_GPU_ID", args.local_rank[0]))

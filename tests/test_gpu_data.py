@@ -50,3 +50,18 @@ def test_gh_batches_match_restatement(tmp_path):
         assert np.abs(xg[:, 0] - xe[:, 0]).max() <= 1e-6
         assert np.abs(xg[:, 1] - xe[:, 1]).max() <= 1e-5
         assert np.array_equal(t.cpu().numpy(), te)
+
+
+def test_h_rgb_batches_match_restatement(tmp_path):
+    """input_type 'H_RGB' (utils/data_utils.py:29-41, 225-226) on the GPU vs the oracle's restatement of
+    separate_stains + combine_stains: within 1e-5. Parity unpinned (skimage absent here)."""
+    root = make_patch_dir(str(tmp_path), per_fold=4, size=32)
+    tr, _ = D.construct_train_valid(root, test_fold=3)
+    ds = D.decode_patch_list(root, tr, patch_mag=200, patch_size=32, cache=False)
+    loader = D.BatchLoader(ds, batch_size=4, shuffle=False, random_flip=True, device="cuda", seed=5,
+                           input_type="H_RGB")
+    for (gb, idx, fl), (x, t) in zip(loader._plan(), loader):
+        xe, te, _ = OD.batch(root, tr[idx], flips=fl, train=True, patch_mag=200, patch_size=32, input_type="H_RGB")
+        assert tuple(x.shape) == xe.shape and xe.shape[1] == 3
+        assert np.abs(x.cpu().numpy() - xe).max() <= 1e-5
+        assert np.array_equal(t.cpu().numpy(), te)
