@@ -1,4 +1,8 @@
-"""Time selunet_bn_bwd_apply at the bench shapes (bs=128 bf16) — profiling tool."""
+"""Time selunet_bn_bwd_apply(_amax) at the bs=128 fp32 shapes (profiling tool).
+
+    python tools/apply_bench.py [--iters 20]
+"""
+import argparse
 import os
 import sys
 
@@ -7,27 +11,37 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from selectivenet_for_semantic_segmentation_binary_amd import _lib as K  # noqa: E402
 
-tot, byt = 0.0, 0
-for c, r in ((64, 256), (128, 128), (256, 64), (512, 32)):
-    m = 128 * r * r
-    dz = torch.randn(m, c, device="cuda").bfloat16()
-    y = torch.randn(m, c, device="cuda").bfloat16()
-    dy = torch.empty_like(dz)
-    v = [torch.rand(c, device="cuda") + 0.5 for _ in range(4)]
-    coef = torch.randn(3, c, device="cuda")
-    f = lambda: K.call("selunet_bn_bwd_apply", K.ptr(dz), K.ptr(y), m, c, *[K.ptr(t) for t in v], K.ptr(coef),  # noqa
-                       K.ptr(dy), K.BF16, K.stream_ptr())
-    for _ in range(3):
-        f()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(10):
-        f()
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / 10
-    tot += ms
-    byt += 3 * m * c * 2
-    print(f"C={c} @{r}: {ms:.3f} ms  {3 * m * c * 2 / ms / 1e6:.0f} GB/s", flush=True)
-print(f"total {tot:.3f} ms  {byt / tot / 1e6:.0f} GB/s")
+SHAPES = [(128 * 256 * 256, 64), (128 * 128 * 128, 128), (128 * 64 * 64, 256), (128 * 32 * 32, 512)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    tot = 0.0
+    for m, c in SHAPES:
+        dz, y = torch.randn(m, c, device="cuda"), torch.randn(m, c, device="cuda")
+        dy = torch.empty_like(dz)
+        co = [torch.rand(c, device="cuda") + 0.5 for _ in range(4)] + [torch.randn(3 * c, device="cuda")]
+        amax = torch.zeros(1, device="cuda")
+
+        def f():
+            K.call("selunet_bn_bwd_apply_amax", K.ptr(dz), K.ptr(y), m, c, *[K.ptr(t) for t in co], K.ptr(dy),
+                   K.ptr(amax), K.F32, K.stream_ptr())
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        tot += ms
+        print(f"apply m={m:9d} C={c:3d}: {ms:.3f} ms  {3 * m * c * 4 / ms / 1e9:7.1f} GB/s", flush=True)
+    print(f"total {tot:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
