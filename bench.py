@@ -9,9 +9,15 @@ data: forward of UNet_B(selective=True), BCEWithLogits aux loss + calc_selective
 global batch of 128 is split into contiguous per-rank chunks (DataParallel semantics), so
 `scaling` is "strong". Rank 0 prints one JSON line.
 
-`value` is the fp32 configuration — the reference's arithmetic (model.py:9-15, train.py:194-209),
-computed with exact-fp32 MFMA products (v_mfma_f32_32x32x2_f32) — timed with no profiling hook
-installed. The same run then measures the bf16 speed configuration (`bf16` key) the same way.
+`value` is the fp32 configuration — the reference's arithmetic (model.py:9-15, train.py:194-209):
+fp32 tensors, statistics, losses and optimizer, with the 3x3 and ConvTranspose2d contractions on
+split-fp16 operands (each fp32 operand = fp16 high + low parts, 22 significant bits; three
+v_mfma_f32_32x32x16_f16 products per fp32 product, fp32 accumulation) — timed with no
+profiling hook installed. The same run then measures the step with every convolution on exact fp32
+MFMA products (`exact_f32` key, v_mfma_f32_32x32x2_f32, SELUNET_X2=0) and the bf16 speed
+configuration (`bf16` key) the same way. `step_mfma_frac` divides the step's direct-convolution
+FLOP rate by the ceiling of the arithmetic actually run: fp16 dense peak / 3 for split-fp16, the
+bf16 peak for `bf16` (none for `exact_f32`: its Winograd kernels execute 2/3 of the direct FLOPs).
 For each configuration, after the headline timing:
   * `roofline`: a separate pass with every kernel entry point bracketed by HIP events on the
     launch stream; the dominant kernel's algorithmic FLOPs (MFMA-bound) or bytes (HBM-bound) per
@@ -48,6 +54,8 @@ from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_bat
 
 TRAIN_GFLOP_PER_IMG_256 = 220.38  # fwd 73.535 x 3 - first-layer dgrad
 PEAK = {"bf16": (2500.0, "TFLOP/s"), "fp32": (157.3, "TFLOP/s")}  # MI355X dense MFMA (MICROARCH guide)
+# ceiling of one fp32 product on split-fp16 operands: three fp16 MFMA products each
+X2_CEILING_TFLOPS = PEAK["bf16"][0] / 3
 HBM_PEAK_GBS = 8000.0
 
 
@@ -475,13 +483,20 @@ def main():
                                      "tools/split_probe.hip), weight gradients likewise"
                        if args.dtype == "fp32" else "bf16 operands, fp32 accumulation"},
             "gpu": torch.cuda.get_device_name(dev),
-            "step_tflops": round(whole, 2), "step_mfma_frac": round(whole / world / PEAK[args.dtype][0], 4),
-            "step_flops_basis": "direct-convolution FLOPs of the training step",
+            "step_tflops": round(whole, 2),
+            "step_mfma_frac": round(whole / world / (X2_CEILING_TFLOPS if args.dtype == "fp32" else PEAK["bf16"][0]), 4),
+            "step_flops_basis": "direct-convolution FLOPs of the training step; ceiling " + (
+                "fp16 dense peak / 3 (split-fp16: three fp16 products per fp32 product)" if args.dtype == "fp32"
+                else "bf16 dense peak"),
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
             "full_loop": head.get("full_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,
         }
         if exact is not None:
+            we = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * exact["value"] / 1e3
+            # (direct-convolution FLOPs: the 1-D Winograd kernels execute 2/3 of them, so no fraction
+            # of the fp32 MFMA peak is quoted for the whole step; roofline.all has each kernel's)
+            exact["step_tflops_direct_equivalent"] = round(we, 2)
             exact["note"] = ("the same fp32 step with every convolution on exact fp32 MFMA products (1-D Winograd "
                              "F(2,3) forward / data-gradient / weight-gradient kernels; SELUNET_X2=0)")
             line["exact_f32"] = exact

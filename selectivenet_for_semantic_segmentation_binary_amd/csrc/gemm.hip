@@ -21,16 +21,6 @@
 
 #include "gemm_common.h"
 
-// SELUNET_GABL: timing ablations of gemm_gather (tools/ablate_gemm; results wrong unless 0):
-// 1 no epilogue store, 2 no MFMAs.
-#ifndef SELUNET_GABL
-#define SELUNET_GABL 0
-#endif
-// SELUNET_GPF: K stages of the gather GEMM in flight in registers (1 or 2)
-#ifndef SELUNET_GPF
-#define SELUNET_GPF 1
-#endif
-
 namespace selunet {
 
 // Persistent over output tiles: workgroup (prow, n_tile) owns column block n_tile and the row tiles
@@ -230,10 +220,6 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
           bh[b] = *reinterpret_cast<const f16x8*>(p + ks * 32);
           bl[b] = *reinterpret_cast<const f16x8*>(p + (2 + ks) * 32);
         }
-#if (SELUNET_GABL & 2)
-        asm volatile("" :: "v"(ah[0]), "v"(al[MT - 1]), "v"(bh[0]), "v"(bl[NT - 1]));
-        continue;
-#endif
 #pragma unroll
         for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -255,14 +241,10 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 #pragma unroll
       for (int b = 0; b < NT; ++b)
         bfr[b] = *reinterpret_cast<const uint4*>(b_src + (wn * WN + b * 32 + l32) * ROWB + boff);
-#if (SELUNET_GABL & 2)
-      asm volatile("" :: "v"(af[0].x ^ af[MT - 1].w), "v"(bfr[0].x ^ bfr[NT - 1].w));
-#else
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < NT; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
-#endif
     }
   };
 
@@ -312,8 +294,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
                             : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
     };
     auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
-    if (!(SELUNET_GABL & 1))
-      lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
+    lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
   };
 
   f32x16 acc[MT][NT];
@@ -330,48 +311,6 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 
   int64_t mt = prow;
   int kc = 0;
-#if SELUNET_GPF == 2
-  // two stages in flight: stage s+2 loads while s multiplies and s+1 (loaded one iteration ago)
-  // waits in registers for its LDS write
-  auto adv = [&](int64_t& m, int& k) {
-    if (k + 1 == nk) {
-      k = 0;
-      m += P;
-    } else {
-      ++k;
-    }
-  };
-  int64_t mt1 = mt;
-  int kc1 = kc;
-  adv(mt1, kc1);
-  Stage n1 = load_stage(total > 1 ? mt1 : mt, total > 1 ? kc1 : kc);
-  for (int64_t s = 0; s < total; ++s) {
-    const bool last_k = kc + 1 == nk;
-    int64_t mt2 = mt1;
-    int kc2 = kc1;
-    adv(mt2, kc2);
-    const bool has2 = s + 2 < total;
-    const Stage n2 = load_stage(has2 ? mt2 : mt, has2 ? kc2 : kc);
-    __builtin_amdgcn_sched_barrier(0);
-    mma_stage(acc, (int)(s & 1));
-    if (last_k) {
-      __syncthreads();
-      epilogue(acc, mt);
-#pragma unroll
-      for (int a = 0; a < MT; ++a)
-#pragma unroll
-        for (int b = 0; b < NT; ++b) acc[a][b] = f32x16{};
-      __syncthreads();
-    }
-    if (s + 1 < total) store_stage(n1, (int)((s + 1) & 1));
-    __syncthreads();
-    n1 = n2;
-    mt = mt1;
-    kc = kc1;
-    mt1 = mt2;
-    kc1 = kc2;
-  }
-#else
   for (int64_t s = 0; s < total; ++s) {
     const bool last_k = kc + 1 == nk;
     const bool more = s + 1 < total;
@@ -396,7 +335,6 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     mt = nmt;
     kc = nkc;
   }
-#endif
   tile_stats_flush<BN, 256>(tile, tid, ts, s1, s2, s3, amx);
 }
 
@@ -1193,10 +1131,7 @@ extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, i
   SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
                   "gemm_gather_x2: every source needs its range word (amax0, amax1)");
   hipStream_t st = as_stream(stream);
-#ifndef SELUNET_X2_BN64
-#define SELUNET_X2_BN64 0
-#endif
-  const bool bn128 = !SELUNET_X2_BN64 && n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
+  const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
   const int64_t P = gather_rows(g, n_cols);
   const float* wcs = w + (int64_t)n_cols * k_pad;
   if (bn128)

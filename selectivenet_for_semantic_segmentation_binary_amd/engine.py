@@ -35,6 +35,14 @@ def _rup(a, b):
     return (a + b - 1) // b * b
 
 
+def fp32_conv_path() -> str:
+    """Which kernels an fp32 training step runs its convolutions on in this process (SELUNET_X2,
+    SELUNET_WINO): "split-fp16" (the default) or "exact-fp32 (Winograd|direct)"."""
+    if os.environ.get("SELUNET_X2", "1") != "0":
+        return "split-fp16"
+    return "exact-fp32 (" + ("direct" if os.environ.get("SELUNET_WINO", "1") == "0" else "Winograd") + ")"
+
+
 @dataclass
 class BNState:
     y: torch.Tensor          # pre-BN conv output (no bias), NHWC [M][C]

@@ -8,6 +8,20 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# one line per fixture run (fixture, fp32 conv path, loss error, worst gradient error, mask flips),
+# printed by tests/conftest.py::pytest_terminal_summary so a quiet run's tail carries them
+SUMMARY = []
+
+
+def format_summary(info):
+    wg = info.get("worst_grad")
+    g = f"worst grad rel-L2 {wg[1]:.2e} ({wg[0]}, {wg[2]})" if wg else "worst grad n/a"
+    flips = info.get("mask_flips")
+    near0 = info.get("near0")
+    m = "mask flips n/a" if flips is None else (
+        f"mask flips {flips}" + (f" (ref logits within 1e-6: {near0})" if near0 is not None else ""))
+    return (f"{info.get('fixture', '?')} [{info.get('path', '?')}]: loss rel err {info.get('loss_rel_err', float('nan')):.2e}, "
+            f"{g}, {m}")
 
 
 def load(name):

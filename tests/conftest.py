@@ -26,3 +26,12 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_terminal_summary(terminalreporter):
+    from tests import _golden as G
+
+    if G.SUMMARY:
+        terminalreporter.section("fixture parity summary")
+        for line in G.SUMMARY:
+            terminalreporter.write_line(line)

@@ -41,7 +41,7 @@ from compute_metric import Evaluator  # noqa: E402  (reference)
 import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch  # noqa: E402
 
-torch.set_num_threads(8)
+torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "8")))
 N_SAMPLES = 128
 
 
@@ -578,7 +578,10 @@ def _sampled(d, name, g):
     return a[d[f"s0/gradidx/{name}"]]
 
 
-def miou_spread(k_members=8, fname="miou_sel_64.npz"):
+MIOU256 = dict(fname="miou_sel_256.npz", n_train=128, n_val=256, size=256, bs=16, epochs=4, lamb=2)
+
+
+def miou_spread(k_members=8, fname="miou_sel_64.npz", **kw):
     """How far apart do two fp32 runs of the reference's own training land? Re-run the mIoU
     fixture's training (miou_fixture) on K copies of the training inputs perturbed at the rounding
     level and record their validation / training mIoU next to the unperturbed run's
@@ -588,7 +591,7 @@ def miou_spread(k_members=8, fname="miou_sel_64.npz"):
     d = dict(np.load(path, allow_pickle=False))
     runs = []
     for k in range(1, k_members + 1):
-        r = miou_fixture(member=k)
+        r = miou_fixture(fname=fname, member=k, **kw)
         m_tr = _miou_cm(r["train_cm"])
         runs.append((float(r["val_miou"]), float(r["val_miou_selective"]), m_tr))
         print(f"member {k}: val mIoU {runs[-1][0]:.5f} selective {runs[-1][1]:.5f} train {m_tr:.5f} "
@@ -598,6 +601,27 @@ def miou_spread(k_members=8, fname="miou_sel_64.npz"):
     d["train_miou_ens"] = np.array([r[2] for r in runs])
     np.savez_compressed(path, **d)
     print(f"wrote {path}: {k_members}-member spread of the reference's mIoU")
+
+
+def miou_collect(k_members, fname):
+    """Fold the members written by `miou256_member k` (run in parallel) into the fixture, as
+    miou_spread does for a sequential run."""
+    path = os.path.join(HERE, fname)
+    d = dict(np.load(path, allow_pickle=False))
+    runs = []
+    for k in range(1, k_members + 1):
+        mp = os.path.join(HERE, f"_miou256_member{k}.npz")
+        r = dict(np.load(mp, allow_pickle=False))
+        runs.append((float(r["val_miou"]), float(r["val_miou_selective"]), _miou_cm(r["train_cm"])))
+    d["val_miou_ens"] = np.array([r[0] for r in runs])
+    d["val_miou_selective_ens"] = np.array([r[1] for r in runs])
+    d["train_miou_ens"] = np.array([r[2] for r in runs])
+    np.savez_compressed(path, **d)
+    for k in range(1, k_members + 1):
+        os.remove(os.path.join(HERE, f"_miou256_member{k}.npz"))
+    sp = np.abs(d["val_miou_ens"] - float(d["val_miou"])).max()
+    sps = np.abs(d["val_miou_selective_ens"] - float(d["val_miou_selective"])).max()
+    print(f"wrote {path}: spread val {sp:.5f} selective {sps:.5f}")
 
 
 def _miou_cm(cm):
@@ -790,6 +814,19 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:2] == ["miou_spread"]:
         miou_spread(int(sys.argv[2]) if len(sys.argv) > 2 else 8)
+        sys.exit(0)
+    if sys.argv[1:] == ["miou256"]:
+        miou_fixture(**MIOU256)
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256_member"]:  # one perturbed member (run several in parallel)
+        k = int(sys.argv[2])
+        r = miou_fixture(member=k, **MIOU256)
+        np.savez(os.path.join(HERE, f"_miou256_member{k}.npz"), **r)
+        print(f"member {k}: val mIoU {float(r['val_miou']):.5f} selective {float(r['val_miou_selective']):.5f} "
+              f"train {_miou_cm(r['train_cm']):.5f}", flush=True)
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256_collect"]:
+        miou_collect(int(sys.argv[2]) if len(sys.argv) > 2 else 8, MIOU256["fname"])
         sys.exit(0)
     if sys.argv[1:] == ["hard"]:
         hard_cases()

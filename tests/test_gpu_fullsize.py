@@ -14,7 +14,10 @@
             loss within 1e-2 relative, every gradient tensor within BF16_GRAD_RL2 relative L2.
 The strict checks are tests/test_gpu_model.py::check_step (logits and losses 1e-4, masks with
 flip reporting, BN buffers, Adam-updated parameters)."""
+import json
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -34,12 +37,41 @@ def _have(fname):
     return os.path.exists(os.path.join(G.GOLDEN, fname))
 
 
-@pytest.mark.parametrize("fname", ["step_sel_n128_256.npz", "step_sel_n16_256.npz", "step_sel_n2_512.npz",
-                                   "step_sel_n8_512.npz"])
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("fname", ["step_sel_n16_256.npz", "step_sel_n2_512.npz", "step_sel_n8_512.npz"])
 def test_full_size_step_matches_reference(fname):
     if not _have(fname):
         pytest.skip(f"{fname} not generated")
     run_fixture(fname)
+
+
+def test_bs128_both_fp32_paths():
+    """The benchmarked shape (config 3: batch 128, 256x256, s_lamb=2) on BOTH fp32 kernel paths
+    against the reference's own step (train.py:194-209, step_sel_n128_256.npz): the default
+    split-fp16 convolutions in this process, and every convolution on exact fp32 MFMA products
+    (SELUNET_X2=0) in a fresh child process (the choice is made when the engine is built; no
+    re-exec of a process that holds the GPU). Both must pass check_step; each path's loss error,
+    worst gradient relative L2 error and mask flips are printed in the run's closing summary
+    (tests/conftest.py). The gate on each path is the fixture's own (check_step: loss and logits
+    1e-4, masks, gradients within max(REF32_GRAD_BOUND, 3 x the reference's perturbation spread))."""
+    fname = "step_sel_n128_256.npz"
+    x2 = run_fixture(fname)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    code = ("import json, sys; sys.path.insert(0, '.');\n"
+            "from tests.test_gpu_model import run_fixture\n"
+            f"info = run_fixture({fname!r})\n"
+            "print('RESULT ' + json.dumps(info))\n")
+    env = dict(os.environ, SELUNET_X2="0")
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    exact = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][len("RESULT "):])
+    G.SUMMARY.append(G.format_summary(exact))
+    print("split-fp16:", G.format_summary(x2))
+    print("exact fp32:", G.format_summary(exact))
+    assert exact["path"].startswith("exact-fp32") and x2["path"] == "split-fp16"
 
 
 @pytest.mark.parametrize("selective", [False, True])

@@ -15,6 +15,7 @@ import torch
 import selectivenet_for_semantic_segmentation_binary_amd as S
 import selectivenet_for_semantic_segmentation_binary_amd.layout as L
 from oracle import unet_b_cpu as O
+from selectivenet_for_semantic_segmentation_binary_amd.engine import fp32_conv_path
 from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
 from tests import _golden as G
 
@@ -68,13 +69,17 @@ def train_step(net, opt, x, lab, selective, lamb, chunks=1):
     return res
 
 
-def check_step(d, s, r, strict):
+def check_step(d, s, r, strict, info=None):
     """Compare one training step's results `r` (loss, coverage, output, grads, params, buffers,
-    num_batches_tracked — numpy) with step `s` of golden fixture `d`; returns failure strings."""
+    num_batches_tracked — numpy) with step `s` of golden fixture `d`; returns failure strings.
+    info (step 0): filled with the loss's relative error, the worst gradient relative L2 error and
+    the number of flipped prediction-mask pixels."""
     selective = bool(d["meta_selective"])
     pre = f"s{s}/"
     tol = 1e-4 if strict else 1e-2
     ref_loss = float(d[pre + "loss"])
+    if info is not None:
+        info["loss_rel_err"] = abs(r["loss"] - ref_loss) / max(1e-30, abs(ref_loss))
     assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
     if selective:
         assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
@@ -100,6 +105,8 @@ def check_step(d, s, r, strict):
         flips, near0 = (0, None) if same else G.mask_flips(d, pre, "output", r["output"], tol)
         print(f"{pre}output mask: {flips} flipped pixels of {mask.size} "
               f"(reference logits within 1e-6 of the boundary: {near0 if near0 is not None else 'n/a'})")
+        if info is not None:
+            info["mask_flips"], info["near0"] = flips, near0
         if not same and near0 == 0:
             assert flips == 0, f"{flips} mask pixels flipped with no reference logit within 1e-6 of the boundary"
     if s == 0 and any(k.startswith("s0/grad64norm/") for k in d.files):
@@ -107,6 +114,8 @@ def check_step(d, s, r, strict):
         f, report = G.check_grads_vs_truth(d, r["grads"], skip=PRE_BN_BIAS)
         print("worst grad errors vs fp64 (ours, reference fp32, perturbed reference):",
               [(n, f"{a:.1e}", f"{b:.1e}", f"{c:.1e}") for n, a, b, c in report[:6]])
+        if info is not None:
+            info["worst_grad"] = (report[0][0], report[0][1], "vs reference fp64")
         fails += f
     elif s == 0:
         # no fp64 run (batch 128 at 256x256 would need ~170 GB of host memory): against the
@@ -114,6 +123,8 @@ def check_step(d, s, r, strict):
         f, report = G.check_grads_vs_ref32(d, r["grads"], REF32_GRAD_BOUND, skip=PRE_BN_BIAS)
         print("worst grad errors vs reference fp32 (samples, norm, reference spread):",
               [(n, f"{a:.1e}", f"{b:.1e}", f"{c:.1e}") for n, a, b, c in report[:6]])
+        if info is not None:
+            info["worst_grad"] = (report[0][0], report[0][1], "vs reference fp32")
         fails += f
     if s == 0:
         # pre-BN conv biases cancel inside training-mode BN: their gradient is 0 up to rounding on
@@ -138,6 +149,9 @@ def check_step(d, s, r, strict):
 
 
 def run_fixture(fname, strict_steps=1):
+    """Run fixture `fname` through the HIP path and check every step (check_step). Returns the
+    step-0 summary (loss error, worst gradient error, mask flips) and records it in G.SUMMARY
+    (printed at the end of the pytest run by tests/conftest.py)."""
     d = G.load(fname)
     n, size = int(d["meta_n"]), int(d["meta_size"])
     selective = bool(d["meta_selective"])
@@ -146,15 +160,19 @@ def run_fixture(fname, strict_steps=1):
     net = build(selective, int(d["meta_seed"]))
     opt = S.Adam(net.parameters(), lr=1e-3)
     xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
-    fails = []
+    fails, info = [], {}
     for s in range(int(d["meta_steps"])):
         r = train_step(net, opt, xt, lt, selective, int(d["meta_lamb"]), int(d["meta_chunks"]))
         r["params"] = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
         bufs = dict(net.named_buffers())
         r["buffers"] = {k: v.cpu().numpy() for k, v in bufs.items()}
         r["num_batches_tracked"] = int(bufs["encoder_layer_1_1.1.num_batches_tracked"])
-        fails += check_step(d, s, r, strict=s < strict_steps)
+        fails += check_step(d, s, r, strict=s < strict_steps, info=info if s == 0 else None)
+    info["path"] = fp32_conv_path()
+    info["fixture"] = fname
+    G.SUMMARY.append(G.format_summary(info))
     assert not fails, "\n".join(fails[:25])
+    return info
 
 
 @pytest.mark.parametrize("fname", ["step_sel_n2_64.npz", "step_nosel_n2_64.npz", "step_sel_lamb8_n3_32.npz",

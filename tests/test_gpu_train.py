@@ -1,9 +1,10 @@
 """Training-loop pieces on the GPU: batch preparation, on-device metrics, the mIoU parity run
-against the reference's own training loop (tests/golden/miou_sel_64.npz, written by
+against the reference's own training loop (tests/golden/miou_sel_256.npz, written by
 tests/golden/make_golden.py from the reference model/loss/Evaluator), and the train.py CLI.
 
 Tolerances: prep and metric counts are integer/byte work -> bit-exact. mIoU: |delta| <= 0.002
-(BASELINE.json north_star) for the fp32 path; the bf16 path is held to 0.01.
+(BASELINE.json north_star) for the fp32 path, training-phase and validation alike; the bf16 path is
+held to 0.01.
 """
 import json
 import os
@@ -96,7 +97,15 @@ def _loop(net, xs, ls, bs, epochs, lamb, training, metrics):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 0.002), (torch.bfloat16, 0.01)])
 def test_miou_parity_vs_reference_training(dtype, tol):
-    d = G.load("miou_sel_64.npz")
+    """BASELINE.json 'mIoU parity': the reference's training loop (train.py:183-241) run by
+    tests/golden/make_golden.py (miou256) — 4 epochs over 128 seeded synthetic 256x256 patches at
+    batch 16, s_lamb=2, Adam lr 1e-3 — then eval-mode mIoU (Evaluator.get_mIoU,
+    utils/compute_metric.py:60-65; prediction rule of train.py:150) over 256 validation patches; the
+    same run through the HIP path must land within `tol` of the reference's training-phase and
+    validation mIoU. The fixture records the reference's own spread (8 runs on training inputs
+    perturbed by 1e-7 relative, `val_miou_ens`), which is below 0.002 at this size, so `tol` is
+    enforced as is."""
+    d = G.load("miou_sel_256.npz")
     size, bs, ep, lamb = int(d["meta_size"]), int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
     xtr, ltr = preprocess(*make_patches(int(d["meta_n_train"]), size, seed=int(d["meta_train_seed"])))
     xva, lva = preprocess(*make_patches(int(d["meta_n_val"]), size, seed=int(d["meta_val_seed"])))
@@ -107,23 +116,22 @@ def test_miou_parity_vs_reference_training(dtype, tol):
     print(f"train loss {losses[0]:.5f}->{losses[-1]:.5f} (reference {ref_losses[0]:.5f}->{ref_losses[-1]:.5f})")
     assert abs(losses[0] - ref_losses[0]) < (1e-4 if dtype == torch.float32 else 2e-2) * abs(ref_losses[0])
     assert np.abs(losses - ref_losses).max() < 0.05 * max(1.0, np.abs(ref_losses).max())
-    tr_cm = tr.confusion_matrix()
-    assert abs(mean_iou(tr_cm) - mean_iou(d["train_cm"])) <= tol
+    m_tr, m_tr_ref = mean_iou(tr.confusion_matrix()), mean_iou(d["train_cm"])
     net.eval()
     vs, vp = SegMetrics(DEV, selective=True, rule="train"), SegMetrics(DEV, selective=False, rule="train")
     with torch.no_grad():
         _loop(net, torch.tensor(xva, device=DEV), torch.tensor(lva, device=DEV), bs, 1, lamb, False, [vs, vp])
     m_sel, m_all = mean_iou(vs.confusion_matrix()), mean_iou(vp.confusion_matrix())
-    print(f"val mIoU {m_all:.5f} (reference {float(d['val_miou']):.5f}), selective {m_sel:.5f} "
-          f"(reference {float(d['val_miou_selective']):.5f})")
-    # The validation mIoU after 40 Adam steps is chaotic: the reference's own fp32 run moves by up
-    # to 0.0079 when its training inputs are perturbed by 1e-7 relative (8 members,
-    # make_golden.py::miou_spread; the training-phase mIoU above moves by 2e-4). The bound is
-    # tol or that spread, whichever is larger.
+    spread = {k: float(np.abs(d[k + "_ens"] - float(d[k])).max()) for k in ("val_miou", "val_miou_selective")
+              if k + "_ens" in d.files}
+    line = (f"mIoU [{dtype}]: train {m_tr:.5f} (reference {m_tr_ref:.5f}), val {m_all:.5f} (reference "
+            f"{float(d['val_miou']):.5f}), val selective {m_sel:.5f} (reference {float(d['val_miou_selective']):.5f}); "
+            f"reference spread {spread}; tol {tol}")
+    print(line)
+    G.SUMMARY.append(line)
+    assert abs(m_tr - m_tr_ref) <= tol
     for got, key in ((m_all, "val_miou"), (m_sel, "val_miou_selective")):
-        ens = d[key + "_ens"] if key + "_ens" in d.files else np.zeros(1)
-        spread = float(np.abs(ens - float(d[key])).max())
-        assert abs(got - float(d[key])) <= max(tol, spread), (key, got, float(d[key]), spread)
+        assert abs(got - float(d[key])) <= tol, (key, got, float(d[key]))
 
 
 def _cli(tmp, *extra):
