@@ -154,9 +154,11 @@ const char* selunet_conv3x3_wino_kernel_name(int32_t n_cols, int32_t mode, int32
  * layer can take it (h, w >= 16, C and c_src0 multiples of 32, C > 32, n_cols a multiple of 64). */
 /* selunet_gemm_gather on split-fp16 operands (ConvTranspose2d forward / data gradient in fp32 training,
  * model.py:44,51,57): w a split-fp16 pack (SELUNET_PACK_CONVT_X2 rows, k_pad == K, K a multiple of 32),
- * amax0 / amax1 the sources' range words; any gather taps and epilogue of selunet_gemm_gather. */
+ * amax0 / amax1 the sources' range words; any gather taps and epilogue of selunet_gemm_gather. Its
+ * statistics slabs have selunet_gemm_gather_x2_stats_rows rows (256-row persistent tiles). */
 int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, int32_t n_cols, int32_t k_pad,
                            const selunet_epilogue* ep, const float* amax0, const float* amax1, void* stream);
+int64_t selunet_gemm_gather_x2_stats_rows(const selunet_gather* a, int32_t n_cols);
 /* selunet_gemm_wgrad_ws_to on split-fp16 operands (the ConvTranspose2d weight gradient in fp32 training,
  * layout SELUNET WG_CONVT = 2, or a Conv2d one, layout 1): vector gathers, K_p and K_q multiples of 64;
  * amax_p0/p1, amax_q0/q1 the sources' range words (p1 / q1 only for two-source gathers). Partials in

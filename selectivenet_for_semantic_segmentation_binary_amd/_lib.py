@@ -100,6 +100,7 @@ SIGNATURES = {
     "selunet_conv3x3_wgrad_x2": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int64, P, P, P, P,
                                            P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
+    "selunet_gemm_gather_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
     "selunet_set_gather_workgroups": (c_int32, [c_int32]),
     "selunet_gemm_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), c_int32, c_int32,

@@ -36,23 +36,25 @@ namespace selunet {
 // and written as fp16 high / low parts into the 128-B K slice (bytes 0-63 high, 64-127 low), B is a
 // split-fp16 pack of the same layout (row unscale factors in wcs), three v_mfma_f32_32x32x16_f16 per
 // 16-k step, accumulators unscaled before the epilogue — as conv3x3_halo_persist_kernel<.., X2>.
-template <typename T, int BN, bool SMALL, bool X2>
-__global__ void __launch_bounds__(256, 2)
+template <typename T, int BN, bool SMALL, bool X2, int BMT = BM, int NTH = 256>
+__global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1)
 gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles, int P,
                    const float* __restrict__ wcs, const float* __restrict__ amax0, const float* __restrict__ amax1) {
   static_assert(!X2 || (std::is_same<T, float>::value && !SMALL), "split-fp16 form: fp32 vector gathers");
   constexpr int E = 16 / sizeof(T);          // elements per 16-B vector
   constexpr int BKE = 128 / sizeof(T);       // K elements per stage
-  constexpr int WN = BN / 2;                 // wave tile columns
+  constexpr int WN = BN / 2;                 // wave tile columns (waves: BMT / 64 rows x 2 columns)
   constexpr int NT = WN / 32;                // 32x32 subtiles per wave (columns)
   constexpr int MT = 2;                      // 64 rows per wave
-  constexpr int AR = BM / 32;                // A rows staged per thread
-  constexpr int BR = BN / 32;                // B rows staged per thread
+  constexpr int RP = NTH / 8;                // rows per staging pass (8 16-B chunks per 128-B row)
+  constexpr int AR = BMT / RP;               // A rows staged per thread
+  constexpr int BR = BN / RP;                // B rows staged per thread
+  static_assert(BMT == 64 * (NTH / 64) / 2, "two wave columns of 64-row waves");
 
-  constexpr int SMEM_MAIN = 2 * (BM + BN) * ROWB, SMEM_EPI = BM * (BN + 4) * 4 + BM * 8;  // (+ row bases)
+  constexpr int SMEM_MAIN = 2 * (BMT + BN) * ROWB, SMEM_EPI = BMT * (BN + 4) * 4 + BMT * 8;  // (+ row bases)
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI];
-  unsigned char* As = smem;                          // [2][BM][ROWB]
-  unsigned char* Bs = smem + 2 * BM * ROWB;          // [2][BN][ROWB]
+  unsigned char* As = smem;                          // [2][BMT][ROWB]
+  unsigned char* Bs = smem + 2 * BMT * ROWB;         // [2][BN][ROWB]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -64,12 +66,12 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   const int n_tile = lb % n_tiles;
   const int64_t prow = lb / n_tiles;
   const int n0 = n_tile * BN;
-  const int64_t m_tiles = (g.M + BM - 1) / BM;
+  const int64_t m_tiles = (g.M + BMT - 1) / BMT;
   const int nk = k_pad / BKE;
   const int64_t total = (m_tiles - prow + P - 1) / P * nk;  // stages of this workgroup (prow < P <= m_tiles)
 
   const int cc = tid & 7;       // 16-B chunk within the 128-B K slice
-  const int rr = tid >> 3;      // base row (0..31)
+  const int rr = tid >> 3;      // base row (0..RP-1)
   float xs = 1.0f;              // X2: operand scale 2^e
   float cfac[NT] = {};          // X2: accumulator unscale per 32-column subtile (this lane's column)
   if constexpr (X2) {
@@ -115,7 +117,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   auto load_stage = [&](int64_t m_tile, int kc) __attribute__((always_inline)) {
     Stage st;
     const int k0 = kc * BKE;
-    const int64_t m0 = m_tile * BM;
+    const int64_t m0 = m_tile * BMT;
     st.ok = 0;
     st.src = 0;
     if constexpr (!SMALL) {
@@ -141,7 +143,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
       }
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        const int64_t m = m0 + rr + 32 * i;
+        const int64_t m = m0 + rr + RP * i;
         const bool rv = m < g.M;
         const unsigned mu = rv ? (unsigned)m : 0u;  // M < 2^31 (host check)
         const unsigned rx = mu % (unsigned)g.w, t = mu / (unsigned)g.w;
@@ -157,7 +159,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         T v[E];
-        const int64_t m = m0 + rr + 32 * i;
+        const int64_t m = m0 + rr + RP * i;
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = from_f<T>(gather_scalar<T>(g, m, k0 + cc * E + e));
         __builtin_memcpy(&st.a[i], v, 16);
@@ -166,14 +168,14 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int n = n0 + rr + 32 * i;
+      const int n = n0 + rr + RP * i;
       st.b[i] = *reinterpret_cast<const uint4*>(B + (int64_t)n * k_pad + k0 + cc * E);
     }
     return st;
   };
 
   auto store_stage = [&](const Stage& st, int buf) __attribute__((always_inline)) {
-    unsigned char* a_dst = As + buf * BM * ROWB;
+    unsigned char* a_dst = As + buf * BMT * ROWB;
     unsigned char* b_dst = Bs + buf * BN * ROWB;
     const SrcArg sa = pick_src(g, st.src);
     if (!SMALL && sa.scale != nullptr) {
@@ -190,19 +192,19 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
         }
         uint4 o;
         __builtin_memcpy(&o, v, 16);
-        put_a(a_dst, rr + 32 * i, o);
+        put_a(a_dst, rr + RP * i, o);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AR; ++i) put_a(a_dst, rr + 32 * i, ((st.ok >> i) & 1u) ? st.a[i] : make_uint4(0, 0, 0, 0));
+      for (int i = 0; i < AR; ++i) put_a(a_dst, rr + RP * i, ((st.ok >> i) & 1u) ? st.a[i] : make_uint4(0, 0, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(b_dst + (rr + 32 * i) * ROWB + cc * 16) = st.b[i];
+      *reinterpret_cast<uint4*>(b_dst + (rr + RP * i) * ROWB + cc * 16) = st.b[i];
   };
 
   auto mma_stage = [&](f32x16 (&acc)[MT][NT], int buf) __attribute__((always_inline)) {
-    const unsigned char* a_src = As + buf * BM * ROWB;
+    const unsigned char* a_src = As + buf * BMT * ROWB;
     const unsigned char* b_src = Bs + buf * BN * ROWB;
     if constexpr (X2) {
 #pragma unroll
@@ -249,16 +251,16 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
   };
 
   // ------------------------------------------------------------------ epilogue (LDS-staged)
-  float* tile = reinterpret_cast<float*>(smem);  // [BM][BN + 4] over the (idle) stage buffers
-  int64_t* rowbase = reinterpret_cast<int64_t*>(smem + BM * (BN + 4) * 4);
+  float* tile = reinterpret_cast<float*>(smem);  // [BMT][BN + 4] over the (idle) stage buffers
+  int64_t* rowbase = reinterpret_cast<int64_t*>(smem + BMT * (BN + 4) * 4);
   const int Cq = N >> 2;
   const TileStats ts = tile_stats(ep, prow, n0, N);
   using Acc = typename StatAcc<T>::type;
-  static_assert(stats_flush_bytes<BN, 256, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
+  static_assert(stats_flush_bytes<BN, NTH, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float amx = 0.0f;  // running max |stored value| (epilogue range word)
   auto epilogue = [&](f32x16 (&acc)[MT][NT], int64_t m_tile) __attribute__((always_inline)) {
-    const int64_t m0 = m_tile * BM;
+    const int64_t m0 = m_tile * BMT;
     if constexpr (X2) {
 #pragma unroll
       for (int a = 0; a < MT; ++a)
@@ -268,7 +270,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     acc_to_lds<MT, NT, BN>(tile, acc, wm * 64, wn * WN, lane);
     // SCATTER2X: each tile row's output base (pixel (img, 2y, 2x) of the 2x-upsampled grid) decoded
     // once into LDS past the tile, instead of three integer divisions per stored 16-B chunk
-    if (ep.mode == SELUNET_EP_SCATTER2X && tid < BM) {
+    if (ep.mode == SELUNET_EP_SCATTER2X && tid < BMT) {
       const int64_t m = m0 + tid;
       int64_t base = -1;
       if (m < g.M) {
@@ -294,7 +296,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
                             : reinterpret_cast<T*>(ep.out1) + m * (N - ep.split) + (col - ep.split);
     };
     auto bias_col = [&](int c) { return ep.mode == SELUNET_EP_SCATTER2X ? (n0 + c) % Cq : n0 + c; };
-    lds_tile_store_acc<T, BM, BN, 256>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
+    lds_tile_store_acc<T, BMT, BN, NTH>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
   };
 
   f32x16 acc[MT][NT];
@@ -335,7 +337,7 @@ gemm_gather_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiAr
     mt = nmt;
     kc = nkc;
   }
-  tile_stats_flush<BN, 256>(tile, tid, ts, s1, s2, s3, amx);
+  tile_stats_flush<BN, NTH>(tile, tid, ts, s1, s2, s3, amx);
 }
 
 // =========================================================================== gemm_wgrad
@@ -1120,6 +1122,33 @@ extern "C" int selunet_conv3x3_wino(const selunet_gather* a, const float* u, int
   return conv3x3_wino_launch(g, u, n_cols, e, as_stream(stream));
 }
 
+// The split-fp16 gather GEMM (ConvTranspose2d forward and data gradient in fp32 training) runs 256 x 128
+// tiles with 512 threads, one persistent workgroup per CU (x2_rows): 1.33x the MACs per staged byte of
+// the 128 x 128 tiles (256 x 256 tiles spill: 696 B of scratch per lane). N not a multiple of 128: the
+// 128 x 64 kernel.
+constexpr int X2_BM = 256;
+
+static int x2_bn(int n_cols, const EpiArg& e) {
+  if (n_cols % 128 != 0 || (e.mode == SELUNET_EP_SPLIT && e.split % 128 != 0)) return 64;
+  return 128;
+}
+
+// statistics slab rows (= persistent row workgroups) of the split-fp16 gather GEMM; independent of
+// the column tile width (128 / 256), like gather_rows. N not a multiple of 128: the 128-row kernel.
+static int64_t x2_rows(const GatherArg& g, int N) {
+  if (N % 128 != 0) return gather_rows(g, N);
+  const int64_t m_tiles = cdiv(g.M, X2_BM);
+  const int64_t wgs = gather_wgs();  // (the gather knob: half as many of these one-per-CU workgroups)
+  if (wgs == 0) return m_tiles;
+  return std::max<int64_t>(1, std::min<int64_t>(m_tiles, std::max<int64_t>(1, wgs / 2) / cdiv(N, 128)));
+}
+
+extern "C" int64_t selunet_gemm_gather_x2_stats_rows(const selunet_gather* a, int32_t n_cols) {
+  GatherArg g;
+  if (make_gather(a, SELUNET_F32, g, 4)) return -1;
+  return x2_rows(g, n_cols);
+}
+
 extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, int32_t n_cols, int32_t k_pad,
                                       const selunet_epilogue* ep, const float* amax0, const float* amax1,
                                       void* stream) {
@@ -1131,15 +1160,16 @@ extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, i
   SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
                   "gemm_gather_x2: every source needs its range word (amax0, amax1)");
   hipStream_t st = as_stream(stream);
-  const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
-  const int64_t P = gather_rows(g, n_cols);
+  const int bn = x2_bn(n_cols, e);
+  const int64_t P = x2_rows(g, n_cols);
   const float* wcs = w + (int64_t)n_cols * k_pad;
-  if (bn128)
-    hipLaunchKernelGGL((gemm_gather_kernel<float, 128, false, true>), dim3((unsigned)(P * (n_cols / 128))), dim3(256),
-                       0, st, g, w, n_cols, k_pad, e, n_cols / 128, (int)P, wcs, amax0, amax1);
+  const dim3 grid((unsigned)(P * (n_cols / bn)));
+  if (bn == 128)
+    hipLaunchKernelGGL((gemm_gather_kernel<float, 128, false, true, X2_BM, 512>), grid, dim3(512), 0, st, g, w,
+                       n_cols, k_pad, e, n_cols / 128, (int)P, wcs, amax0, amax1);
   else
-    hipLaunchKernelGGL((gemm_gather_kernel<float, 64, false, true>), dim3((unsigned)(P * (n_cols / 64))), dim3(256), 0,
-                       st, g, w, n_cols, k_pad, e, n_cols / 64, (int)P, wcs, amax0, amax1);
+    hipLaunchKernelGGL((gemm_gather_kernel<float, 64, false, true>), grid, dim3(256), 0, st, g, w, n_cols, k_pad, e,
+                       n_cols / 64, (int)P, wcs, amax0, amax1);
   return check_launch("gemm_gather_x2");
 }
 

@@ -627,7 +627,8 @@ class Engine:
         K.marker(("grads", name))
         dz = K.keep(torch.empty(n * h * w, ci, dtype=self.dt, device=dev))
         ga = K.gather(n, h, w, 4, K.source(du.t, co))
-        rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
+        rows = (K.query("selunet_gemm_gather_x2_stats_rows", ga, ci) if wp.mode == "x2"
+                else K.query("selunet_gemm_stats_rows", ga, ci, self.code))
         slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = bnb_for(prev, slab)

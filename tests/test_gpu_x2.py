@@ -322,7 +322,7 @@ def test_x2_convT_fwd_dgrad(cin, cout, gwgs, gather_wgs):
     sc, sh = (gen(cin, seed=43).abs() + 0.5).to(DEV), (gen(cin, seed=44) * 0.3).to(DEV)
     mean, invstd = (gen(cin, seed=45) * 0.1).to(DEV), (gen(cin, seed=46).abs() + 0.5).to(DEV)
     g4 = K.gather(n, h, w, 4, K.source(dud, cout))
-    rows = K.query("selunet_gemm_stats_rows", g4, cin, K.F32)
+    rows = K.query("selunet_gemm_gather_x2_stats_rows", g4, cin)
     slab = torch.empty(rows, 3, cin, device=DEV)
     ep = K.Epilogue(K.ptr(da), None, None, None, K.EP_PLAIN, 0)
     ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
