@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=3, help="steps of the per-kernel attribution pass")
     ap.add_argument("--no-full-loop", action="store_true")
+    ap.add_argument("--no-input-loop", action="store_true", help="skip the timed loop fed by the patch loader")
     ap.add_argument("--layer-report", action="store_true", help="print per-entry-point timing to stderr")
     return ap.parse_args()
 
@@ -314,15 +315,15 @@ def run_config(args, dtype, world, rank, dev, xt, lt, local_batch):
     loss_a = S.BCEWithLogitsLoss()
     state = {}
 
-    def step():
+    def step(x=xt, t=lt):
         if selective:
-            out, sel, aux = net(xt)
-            loss = loss_a(aux, lt)
-            sel_loss, _ = S.calc_selective_risk_image_b(out, sel, target=lt, lamb=args.lamb)
+            out, sel, aux = net(x)
+            loss = loss_a(aux, t)
+            sel_loss, _ = S.calc_selective_risk_image_b(out, sel, target=t, lamb=args.lamb)
             loss = loss + sel_loss
         else:
-            out, sel = net(xt), None
-            loss = loss_a(out, lt)
+            out, sel = net(x), None
+            loss = loss_a(out, t)
         opt.zero_grad()
         loss.backward()
         opt.step()
@@ -371,12 +372,62 @@ def run_config(args, dtype, world, rank, dev, xt, lt, local_batch):
         res["full_loop"] = {"value": round(args.batch * args.steps / el, 2), "ms_per_step": round(1e3 * el / args.steps, 3),
                             "includes": "step + SegMetrics.add_batch (thresholded masks, 2x2 confusion matrix, "
                                         "rejection counts) + loss sums, read back once"}
+        if not args.no_input_loop and world == 1 and dtype == args.dtype:
+            res["input_loop"] = input_loop(args, dev, step, state, selective)
     res["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
     del net, opt, state, step
     gc.collect()
     torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
     return res
+
+
+def input_loop(args, dev, step, state, selective):
+    """The training loop fed by the patch loader instead of HBM-resident tensors (train.py:183-191 +
+    utils/data_utils.py:200-236 restated): data.BatchLoader gathers each shuffled global batch of
+    uint8 NHWC patches into pinned host memory on a prefetch thread, copies it to the GPU (uint8:
+    4x fewer bytes than the reference's fp32 input) and expands it there (selunet_prep_batch_mode:
+    /255, Normalization, RandomFlip, NCHW fp32, label truncation); then the step and the on-device
+    metrics. Synthetic patches (2 global batches, cycled over epochs). Also times the reference's
+    own per-step input copy, the pageable fp32 [B,3,H,W] tensor .to(cuda) of train.py:186."""
+    from selectivenet_for_semantic_segmentation_binary_amd import data as D
+
+    ds = D.synthetic_patchset(2 * args.batch, args.size, seed=5)
+    loader = D.BatchLoader(ds, args.batch, shuffle=True, random_flip=True, device=dev)
+    ev = SegMetrics(dev, selective=selective, rule="train")
+    epoch = [0]
+
+    def run(nsteps):
+        done = 0
+        while done < nsteps:
+            loader.set_epoch(epoch[0])
+            epoch[0] += 1
+            for x, t in loader:
+                step(x, t)
+                ev.add_batch(state["out"].detach(), t, None if state["sel"] is None else state["sel"].detach())
+                done += 1
+                if done == nsteps:
+                    break
+        ev.raw()
+
+    run(2)
+    el = timed(lambda: run(args.steps), 1, 1, dev)
+    # the reference's input copy: pageable fp32 NCHW batch -> GPU (train.py:186)
+    xh = torch.empty(args.batch, 3, args.size, args.size, dtype=torch.float32)
+    xh.fill_(0.5)
+    xh.to(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        xh.to(dev)
+    torch.cuda.synchronize()
+    h2d = (time.perf_counter() - t0) / 5
+    return {"value": round(args.batch * args.steps / el, 2), "ms_per_step": round(1e3 * el / args.steps, 3),
+            "includes": "data.BatchLoader (shuffled uint8 NHWC patches gathered into pinned memory on a prefetch "
+                        "thread, H2D copy as uint8, GPU normalise / flips / NCHW fp32) + step + SegMetrics",
+            "reference_fp32_h2d_ms": round(1e3 * h2d, 3),
+            "reference_fp32_h2d_note": f"pageable fp32 [{args.batch},3,{args.size},{args.size}] .to(cuda) per step "
+                                       f"(train.py:186), {xh.numel() * 4 / 1e6:.1f} MB; not in any timed value"}
 
 
 def roofline(args, dtype, timer, ksteps, kel, local_batch):
@@ -489,7 +540,7 @@ def main():
                 "fp16 dense peak / 3 (split-fp16: three fp16 products per fp32 product)" if args.dtype == "fp32"
                 else "bf16 dense peak"),
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
-            "full_loop": head.get("full_loop"),
+            "full_loop": head.get("full_loop"), "input_loop": head.get("input_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,
         }
         if exact is not None:

@@ -1160,6 +1160,8 @@ extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, i
   SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
                   "gemm_gather_x2: every source needs its range word (amax0, amax1)");
   hipStream_t st = as_stream(stream);
+  // the ConvTranspose2d forward (scatter epilogue): the resident-weight kernel (convt.hip)
+  if (convt_x2_eligible(g, n_cols, e)) return convt_x2_launch(g, w, n_cols, e, amax0, st);
   const int bn = x2_bn(n_cols, e);
   const int64_t P = x2_rows(g, n_cols);
   const float* wcs = w + (int64_t)n_cols * k_pad;

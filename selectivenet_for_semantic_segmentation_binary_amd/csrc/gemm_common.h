@@ -431,6 +431,10 @@ bool conv3x3_x2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
 bool conv3x3_x2_eligible(const GatherArg& g, int N);
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st);
+// ConvTranspose2d forward on split-fp16 operands with resident weights (convt.hip)
+bool convt_x2_eligible(const GatherArg& g, int N, const EpiArg& e);
+int convt_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
+                    hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,

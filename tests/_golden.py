@@ -185,3 +185,22 @@ def mask_flips(d, pre, head, logits, tol):
     if flips:
         assert at[diff].max() <= 2 * tol * absmax, (head, flips, float(at[diff].max()), absmax)
     return flips, near0
+
+
+def grad_errors(d, grads, skip=()):
+    """Per tensor, the relative L2 error of `grads` on the fixture's samples against its truth: the
+    fp64 step where the fixture has one, the reference's fp32 step otherwise (batch 128)."""
+    has64 = any(k.startswith("s0/grad64norm/") for k in d.files)
+    out = {}
+    for name in tensor_keys(d, "s0/grad"):
+        if name in skip:
+            continue
+        a = np.asarray(grads[name], np.float64).ravel()
+        full = "s0/gradfull/" + name in d.files
+        if has64:
+            ref = d[("s0/grad64full/" if full else "s0/grad64val/") + name].astype(np.float64)
+        else:
+            ref = d[("s0/gradfull/" if full else "s0/gradval/") + name].astype(np.float64)
+        got = a if full else a[d["s0/gradidx/" + name]]
+        out[name] = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
+    return out

@@ -578,7 +578,7 @@ def _sampled(d, name, g):
     return a[d[f"s0/gradidx/{name}"]]
 
 
-MIOU256 = dict(fname="miou_sel_256.npz", n_train=128, n_val=256, size=256, bs=16, epochs=4, lamb=2)
+MIOU256 = dict(fname="miou_sel_256.npz", n_train=128, n_val=256, size=256, bs=16, epochs=16, lamb=2)
 
 
 def miou_spread(k_members=8, fname="miou_sel_64.npz", **kw):
@@ -748,6 +748,48 @@ def augment_ensemble(fname, k_members=8, ckpt=False):
     print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB) with the {k_members}-member perturbation ensemble")
 
 
+def augment_bf16ref(fname):
+    """The reference's own step run in bf16: the reference UNet_B forward under
+    torch.autocast("cpu", dtype=torch.bfloat16) (convolutions with bf16 operands, as a user would
+    enable mixed precision on the reference), outputs cast back to fp32 for the losses, then the
+    backward. Per tensor, the relative L2 error of its gradient against the fixture's fp64 truth
+    (the reference's fp32 step where the fixture has none: batch 128) (`s0/grad_bf16ref/<name>`)
+    and its loss (`s0/loss_bf16ref`): the bf16 speed configuration of the
+    HIP path is held to no worse than this (tests/test_gpu_fullsize.py)."""
+    path = os.path.join(HERE, fname)
+    d = dict(np.load(path, allow_pickle=False))
+    n, size = int(d["meta_n"]), int(d["meta_size"])
+    selective, lamb, seed = bool(d["meta_selective"]), int(d["meta_lamb"]), int(d["meta_seed"])
+    x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
+    net = build_ref(seed, selective)
+    names = {id(p): k for k, p in net.named_parameters()}
+    has64 = any(k.startswith("s0/grad64norm/") for k in d)
+    if not has64:  # batch 128: checkpointed sub-modules (memory), truth = the reference's fp32 step
+        checkpoint_modules(net)
+    net.train()
+    xt, lt = torch.tensor(x), torch.tensor(lab)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        outs = net(xt)
+    outs = tuple(o.float() for o in outs) if selective else (outs.float(),)
+    loss_A = torch.nn.BCEWithLogitsLoss()
+    if selective:
+        loss = loss_A(outs[2], lt) + ref_loss.calc_selective_risk_image_b(outs[0], outs[1], target=lt, lamb=lamb)[0]
+    else:
+        loss = loss_A(outs[0], lt)
+    loss.backward()
+    d["s0/loss_bf16ref"] = np.float64(loss.item())
+    for p in net.parameters():
+        nm = names[id(p)]
+        g = _sampled(d, nm, p.grad)
+        if has64:
+            ref = (d[f"s0/grad64full/{nm}"] if f"s0/grad64full/{nm}" in d else d[f"s0/grad64val/{nm}"]).astype(np.float64)
+        else:
+            ref = (d[f"s0/gradfull/{nm}"] if f"s0/gradfull/{nm}" in d else d[f"s0/gradval/{nm}"]).astype(np.float64)
+        d["s0/grad_bf16ref/" + nm] = np.float64(np.linalg.norm(g - ref) / max(np.linalg.norm(ref), 1e-30))
+    np.savez_compressed(path, **d)
+    print(f"wrote {path}: reference bf16-autocast step, loss {loss.item():.6f} (fp32 {float(d['s0/loss']):.6f})")
+
+
 def check_checkpointing(n=2, size=32):
     """The checkpointed reference step equals the plain one (same modules, same arithmetic)."""
     x, lab = make_batch(n, size, seed=1)
@@ -827,6 +869,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:2] == ["miou256_collect"]:
         miou_collect(int(sys.argv[2]) if len(sys.argv) > 2 else 8, MIOU256["fname"])
+        sys.exit(0)
+    if sys.argv[1:2] == ["bf16ref"]:
+        for f in sys.argv[2:]:
+            augment_bf16ref(f)
         sys.exit(0)
     if sys.argv[1:] == ["hard"]:
         hard_cases()

@@ -30,7 +30,12 @@ from tests.test_gpu_model import PRE_BN_BIAS, build, run_fixture, train_step
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-BF16_GRAD_RL2 = 0.1  # measured worst 0.073 (decoder_layer_4_2 bias, bs=128): bf16 operand rounding is 2^-8
+# bf16 vs the fp32 HIP path, non-selective UNet_B (configs[1]; no reference bf16 run of that model is
+# recorded): measured worst 0.073. The selective model is held per tensor to the reference's own
+# bf16 arithmetic instead (test_bf16_step_vs_reference_bf16).
+BF16_GRAD_RL2 = 0.1
+# per tensor: HIP bf16 error <= BF16_REF_FACTOR x the reference's bf16-autocast error (+ floor)
+BF16_REF_FACTOR, BF16_FLOOR = 3.0, 2e-3
 
 
 def _have(fname):
@@ -104,3 +109,48 @@ def test_bf16_bs128_tracks_fp32(selective):
     print(f"bf16 vs fp32 (selective={selective}): loss {b['loss']:.6f} vs {a['loss']:.6f}, "
           f"logits rel-L2 {lrel:.2e}, worst grad rel-L2 {[(f'{e:.2e}', k) for e, k in worst[:5]]}")
     assert worst[0][0] <= BF16_GRAD_RL2, worst[:5]
+
+
+@pytest.mark.parametrize("fname", ["step_sel_n2_64.npz", "step_sel_n16_256.npz", "step_sel_n128_256.npz"])
+def test_bf16_step_vs_reference_bf16(fname):
+    """The bf16 speed configuration (bf16 operands, fp32 accumulation and statistics) against the
+    reference's own step run in bf16: the reference UNet_B forward under torch.autocast(bf16) on
+    the same batch and weights (tests/golden/make_golden.py bf16ref: per tensor its gradient error
+    `s0/grad_bf16ref/<name>` against the fixture's truth — fp64, or the reference's fp32 step at batch
+    128). Per tensor the HIP bf16 gradient's error against the same truth must be within
+    BF16_REF_FACTOR x the reference's bf16 error (floor BF16_FLOOR): the bound follows the bf16
+    operand rounding of the reference's own arithmetic rather than a flat tolerance (the reference's
+    bf16 error spans 3e-4 .. 0.08 over the tensors at batch 128, 1e-3 .. 0.5 at 2x64x64)."""
+    if not _have(fname):
+        pytest.skip(f"{fname} not generated")
+    d = G.load(fname)
+    if not any(k.startswith("s0/grad_bf16ref/") for k in d.files):
+        pytest.skip(f"{fname} has no reference bf16 run")
+    n, size = int(d["meta_n"]), int(d["meta_size"])
+    x, lab = make_batch(n, size, seed=int(d["meta_data_seed"]))
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    del x
+    net = build(True, int(d["meta_seed"]), dtype=torch.bfloat16)
+    opt = S.Adam(net.parameters(), lr=1e-3)
+    r = train_step(net, opt, xt, lt, True, int(d["meta_lamb"]))
+    has64 = any(k.startswith("s0/grad64norm/") for k in d.files)
+    truth_loss = float(d["s0/loss64"]) if has64 else float(d["s0/loss"])
+    ref_bf = float(d["s0/loss_bf16ref"])
+    assert abs(r["loss"] - truth_loss) <= max(BF16_REF_FACTOR * abs(ref_bf - truth_loss), 1e-4 * abs(truth_loss)), \
+        (r["loss"], ref_bf, truth_loss)
+    errs = G.grad_errors(d, r["grads"], skip=PRE_BN_BIAS)
+    rows, fails = [], []
+    for k, e in errs.items():
+        eref = float(d["s0/grad_bf16ref/" + k])
+        b = max(BF16_REF_FACTOR * eref, BF16_FLOOR)
+        rows.append((e / b, e, eref, k))
+        if e > b:
+            fails.append(f"{k}: {e:.3e} > {b:.3e} (reference bf16 {eref:.3e})")
+    rows.sort(reverse=True)
+    worst = rows[0]
+    G.SUMMARY.append(f"{fname} [bf16]: loss {r['loss']:.6f} (reference bf16 {ref_bf:.6f}, truth {truth_loss:.6f}); "
+                     f"worst grad rel-L2 {worst[1]:.2e} on {worst[3]} vs reference bf16 {worst[2]:.2e} "
+                     f"(ratio to bound {worst[0]:.2f}); median ours {np.median([x[1] for x in rows]):.2e} / "
+                     f"reference bf16 {np.median([x[2] for x in rows]):.2e}")
+    print(G.SUMMARY[-1])
+    assert not fails, "\n".join(fails[:20])

@@ -98,7 +98,7 @@ def _loop(net, xs, ls, bs, epochs, lamb, training, metrics):
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 0.002), (torch.bfloat16, 0.01)])
 def test_miou_parity_vs_reference_training(dtype, tol):
     """BASELINE.json 'mIoU parity': the reference's training loop (train.py:183-241) run by
-    tests/golden/make_golden.py (miou256) — 4 epochs over 128 seeded synthetic 256x256 patches at
+    tests/golden/make_golden.py (miou256) — 16 epochs over 128 seeded synthetic 256x256 patches at
     batch 16, s_lamb=2, Adam lr 1e-3 — then eval-mode mIoU (Evaluator.get_mIoU,
     utils/compute_metric.py:60-65; prediction rule of train.py:150) over 256 validation patches; the
     same run through the HIP path must land within `tol` of the reference's training-phase and

@@ -47,6 +47,9 @@ def main():
         out = torch.empty(n * 4 * r * r, co, device=dev, dtype=dt)
         g = K.gather(n, r, r, 1, K.source(x, ci, sc, sh))
         ep = K.Epilogue(K.ptr(out), None, K.ptr(bias), None, K.EP_SCATTER2X, 0)
+        amo = torch.zeros(1, device=dev)
+        if a.x2:
+            ep.amax = K.ptr(amo)  # the up-sampled tensor's range word, as in the step
         if a.x2:
             f = lambda: K.call("selunet_gemm_gather_x2", g, K.ptr(w), 4 * co, ci, ep, K.ptr(amax), None,  # noqa: E731
                                K.stream_ptr())
@@ -63,6 +66,12 @@ def main():
         dz = torch.empty(n * r * r, ci, device=dev, dtype=dt)
         gd = K.gather(n, r, r, 4, K.source(du, co))
         epd = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
+        if a.x2:  # as in the training step: the BN-backward sums of the producer layer in the epilogue
+            yprev = torch.randn(n * r * r, ci, device=dev)
+            bn_c = [torch.rand(ci, device=dev) + 0.5 for _ in range(4)]
+            rows = K.query("selunet_gemm_gather_x2_stats_rows", gd, ci)
+            slab = torch.empty(rows, 3, ci, device=dev)
+            epd.bnb = K.BnBwdStats(K.ptr(yprev), *(K.ptr(t) for t in bn_c), K.ptr(slab))
         if a.x2:
             fd = lambda: K.call("selunet_gemm_gather_x2", gd, K.ptr(wd), ci, 4 * co, epd, K.ptr(amax), None,  # noqa: E731
                                 K.stream_ptr())

@@ -1,0 +1,86 @@
+"""How chaotic is the validation mIoU of a short training run? (profiling / study tool, GPU)
+
+Trains the HIP SelectiveUNet_B (fp32, split-fp16 convolutions) with the reference's loop
+(train.py:183-241: BCEWithLogits aux + calc_selective_risk_image_b, Adam) on seeded synthetic
+patches, K times with the training inputs perturbed by 1e-7 relative (member 0 unperturbed), and
+prints each member's training-phase and eval-mode validation mIoU and the spread — the quantity
+tests/golden/make_golden.py::miou_spread measures on the reference, found here in seconds per run.
+
+    python tools/miou_spread_gpu.py --n-train 128 --n-val 256 --size 256 --bs 16 --epochs 4 --lr 1e-3 -k 8
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import selectivenet_for_semantic_segmentation_binary_amd as S  # noqa: E402
+import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics, mean_iou  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess  # noqa: E402
+
+
+def run(xtr, ltr, xva, lva, a, member):
+    if member:
+        rng = np.random.Generator(np.random.PCG64(1000 + member))
+        xtr = (xtr.astype(np.float64) * (1.0 + 1e-7 * rng.standard_normal(xtr.shape))).astype(np.float32)
+    dev = "cuda"
+    net = S.UNet_B("RGB", selective=True)
+    p = L.seeded_params(0, "RGB", True)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    net = net.to(dev).train()
+    opt = S.Adam(net.parameters(), lr=a.lr)
+    loss_a = S.BCEWithLogitsLoss()
+    xt, lt = torch.tensor(xtr, device=dev), torch.tensor(ltr, device=dev)
+    tr = SegMetrics(dev, selective=True, rule="train")
+    for ep in range(a.epochs):
+        if a.lr_decay and ep == a.epochs // 2:
+            for g in opt.param_groups:
+                g["lr"] = a.lr * a.lr_decay
+        for b0 in range(0, xt.shape[0], a.bs):
+            x, lab = xt[b0:b0 + a.bs], lt[b0:b0 + a.bs]
+            o, s, ax = net(x)
+            loss = loss_a(ax, lab) + S.calc_selective_risk_image_b(o, s, target=lab, lamb=a.lamb)[0]
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            tr.add_batch(o.detach(), lab, s.detach())
+    net.eval()
+    vp = SegMetrics(dev, selective=False, rule="train")
+    xv, lv = torch.tensor(xva, device=dev), torch.tensor(lva, device=dev)
+    with torch.no_grad():
+        for b0 in range(0, xv.shape[0], a.bs):
+            o, s, _ = net(xv[b0:b0 + a.bs])
+            vp.add_batch(o, lv[b0:b0 + a.bs], s)
+    return mean_iou(tr.confusion_matrix()), mean_iou(vp.confusion_matrix()), float(loss.item())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-train", type=int, default=128)
+    ap.add_argument("--n-val", type=int, default=256)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--bs", type=int, default=16)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--lr-decay", type=float, default=0.0, help="multiply lr by this at half the epochs")
+    ap.add_argument("--lamb", type=float, default=2)
+    ap.add_argument("-k", type=int, default=8)
+    a = ap.parse_args()
+    xtr, ltr = preprocess(*make_patches(a.n_train, a.size, seed=2024))
+    xva, lva = preprocess(*make_patches(a.n_val, a.size, seed=2025))
+    res = [run(xtr, ltr, xva, lva, a, m) for m in range(a.k + 1)]
+    tr = np.array([r[0] for r in res])
+    va = np.array([r[1] for r in res])
+    print(f"cfg {vars(a)}")
+    print("train mIoU", np.round(tr, 5), "val mIoU", np.round(va, 5), "final loss", [round(r[2], 4) for r in res])
+    print(f"SPREAD train {np.abs(tr[1:] - tr[0]).max():.5f} val {np.abs(va[1:] - va[0]).max():.5f} "
+          f"val range {va.max() - va.min():.5f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
