@@ -104,6 +104,10 @@ typedef struct selunet_epilogue {
   /* nullable: max |stored value| folded into *amax with an atomic max (float bits; the caller zeroes
    * it): the range word of a split-fp16 operand (selunet_conv3x3_x2) read by the next layer. */
   float* amax;
+  /* nullable, with stats: per-column shift c (the previous step's batch mean): stats then hold the sums
+   * of (v - c) and (v - c)^2, which selunet_bn_stats_finalize_shifted turns into the mean and a
+   * one-pass variance that loses ~eps * (mean - c)^2 / var instead of ~eps * mean^2 / var. */
+  const float* stats_center;
 } selunet_epilogue;
 
 const char* selunet_last_error(void);
@@ -320,6 +324,19 @@ int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const floa
 int selunet_bn_centered_partials_adaptive(const void* y, int64_t m, int32_t c, const float* center,
                                           const float* uvar, float ratio, float* slab, int32_t dtype,
                                           void* stream);
+/* First pass of the fp32 batch statistics from a slab of SHIFTED sums (selunet_epilogue.stats_center =
+ * center, the previous step's batch mean): mean = center + E[y - center]; uvar_flag[c] = the unbiased
+ * one-pass variance, or -1 where (mean - center)^2 > ratio * var (there it loses digits); center is
+ * then overwritten with mean (the next step's center). invstd / scale / shift are provisional (eps
+ * 1e-5, no running-statistic update). Followed by selunet_bn_centered_partials_adaptive(center = mean,
+ * uvar = uvar_flag, ratio = +inf: re-reads exactly the flagged channel groups) and
+ * selunet_bn_stats_finalize_centered, whose outputs are final. In training the previous batch mean
+ * differs from the current one by a small fraction of the standard deviation, so after the first
+ * step almost no channel group is re-read. */
+int selunet_bn_stats_finalize_shifted(const float* slab, int64_t rows, double* ws, int64_t count, int32_t c,
+                                      float* center, const float* conv_bias, const float* gamma,
+                                      const float* beta, float ratio, float* mean, float* uvar_flag,
+                                      float* invstd, float* scale, float* shift, void* stream);
 int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums,
                                        int64_t count, int32_t c, const float* center,
                                        const float* conv_bias, const float* gamma, const float* beta,
@@ -368,6 +385,10 @@ int selunet_im2col3x3(const float* x, int32_t n, int32_t c, int32_t h, int32_t w
  * column statistics of selunet_gemm_gather (stats [selunet_first_conv_rows][2][64], nullable).
  * wpack: the conv weight from selunet_pack_conv3x3 with k_pad = 32. */
 int64_t selunet_first_conv_rows(int32_t n, int32_t h, int32_t w);
+/* selunet_first_conv_fwd with its statistics shifted by center (selunet_epilogue.stats_center). */
+int selunet_first_conv_fwd_centered(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w,
+                                    const void* wpack, void* y, float* stats, const float* center,
+                                    int32_t dtype, void* stream);
 int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* wpack,
                            void* y, float* stats, int32_t dtype, void* stream);
 /* Its weight gradient: slab [selunet_first_conv_wgrad_rows][64][32] of per-workgroup partial sums

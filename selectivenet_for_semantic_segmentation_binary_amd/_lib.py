@@ -41,7 +41,7 @@ class BnBwdStats(ctypes.Structure):
 class Epilogue(ctypes.Structure):
     _fields_ = [("out0", c_void_p), ("out1", c_void_p), ("bias", c_void_p), ("stats", c_void_p),
                 ("mode", c_int32), ("split", c_int32), ("colsum", c_void_p), ("bnb", BnBwdStats),
-                ("amax", c_void_p)]
+                ("amax", c_void_p), ("stats_center", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -130,6 +130,9 @@ SIGNATURES = {
     "selunet_maxpool2_bwd_slab_rows": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
     "selunet_first_conv_rows": (c_int64, [c_int32, c_int32, c_int32]),
     "selunet_first_conv_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
+    "selunet_first_conv_fwd_centered": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, c_int32, P]),
+    "selunet_bn_stats_finalize_shifted": (c_int32, [P, c_int64, P, c_int64, c_int32, P, P, P, P, c_float, P, P, P, P,
+                                                    P, P]),
     "selunet_first_conv_wgrad_rows": (c_int64, [c_int32, c_int32, c_int32]),
     "selunet_first_conv_wgrad": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, c_int32, P]),
     "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),

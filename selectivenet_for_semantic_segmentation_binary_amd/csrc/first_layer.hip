@@ -275,13 +275,16 @@ extern "C" int64_t selunet_first_conv_rows(int32_t n, int32_t h, int32_t w) {
   return tiles_of(n, h, w, tx, ty);
 }
 
-extern "C" int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* wpack,
-                                      void* y, float* stats, int32_t dtype, void* stream) {
+extern "C" int selunet_first_conv_fwd_centered(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w,
+                                               const void* wpack, void* y, float* stats, const float* center,
+                                               int32_t dtype, void* stream) {
   SELUNET_REQUIRE(x && wpack && y && n > 0 && h > 0 && w > 0 && cin >= 1 && cin <= 3, "first_conv_fwd: bad arguments");
   SELUNET_REQUIRE((int64_t)n * cdiv(h, FT) * cdiv(w, FT) < (int64_t(1) << 31), "first_conv_fwd: grid too large");
   int tx, ty;
   const int tiles = tiles_of(n, h, w, tx, ty);
-  EpiArg ep{y, nullptr, nullptr, stats, SELUNET_EP_PLAIN, 0, nullptr, BnBwdArg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}};
+  SELUNET_REQUIRE(center == nullptr || stats != nullptr, "first_conv_fwd: center only with stats");
+  EpiArg ep{y, nullptr, nullptr, stats, SELUNET_EP_PLAIN, 0, nullptr,
+            BnBwdArg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, nullptr, center};
   const unsigned blocks = (unsigned)std::min(tiles, 2048);  // 8 tiles in flight per CU pair of workgroups
   if (dtype == SELUNET_F32)
     hipLaunchKernelGGL(first_conv_fwd_kernel<float>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h, w,
@@ -292,6 +295,11 @@ extern "C" int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, in
   else
     return fail(SELUNET_EINVAL, "first_conv_fwd: bad dtype %d", dtype);
   return check_launch("first_conv_fwd");
+}
+
+extern "C" int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* wpack,
+                                      void* y, float* stats, int32_t dtype, void* stream) {
+  return selunet_first_conv_fwd_centered(x, n, cin, h, w, wpack, y, stats, nullptr, dtype, stream);
 }
 
 extern "C" int64_t selunet_first_conv_wgrad_rows(int32_t n, int32_t h, int32_t w) {

@@ -1073,7 +1073,8 @@ static int check_gather_call(const selunet_gather* a, const void* b, int32_t n_c
                         bb.invstd && ep->bias == nullptr,
                     "bn-backward sums need the plain epilogue without stats/bias and y/scale/shift/mean/invstd");
   e = EpiArg{ep->out0, ep->out1, ep->bias, ep->stats, ep->mode, ep->split, ep->colsum,
-             BnBwdArg{bb.y, bb.scale, bb.shift, bb.mean, bb.invstd, bb.slab}, ep->amax};
+             BnBwdArg{bb.y, bb.scale, bb.shift, bb.mean, bb.invstd, bb.slab}, ep->amax, ep->stats_center};
+  SELUNET_REQUIRE(ep->stats_center == nullptr || ep->stats != nullptr, "stats_center only with stats");
   return SELUNET_OK;
 }
 

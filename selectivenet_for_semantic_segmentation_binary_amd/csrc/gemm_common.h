@@ -174,6 +174,7 @@ struct EpiArg {
   float* colsum;
   BnBwdArg bnb;
   float* amax;  // nullable: atomic max of |stored value| (float bits), see selunet_epilogue.amax
+  const float* stats_center;  // nullable: stats are sums of (v - center), (v - center)^2
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -219,6 +220,7 @@ struct TileStats {
   BnBwdArg bnb;        // scale/shift/mean/invstd/slab offset to gcol0; y = base pointer
   const void* out0;    // base of the PLAIN output (to locate y)
   float* amax;         // nullable: running max |stored value| (atomic, float bits)
+  const float* center; // nullable: stats shift per column, offset to gcol0
 };
 
 // The statistics outputs of workgroup (slab row `row`, first global column n0) of an N-column GEMM.
@@ -239,6 +241,7 @@ __device__ __forceinline__ TileStats tile_stats(const EpiArg& ep, int64_t row, i
   }
   ts.out0 = ep.out0;
   ts.amax = ep.amax;
+  ts.center = ep.stats_center ? ep.stats_center + n0 : nullptr;
   return ts;
 }
 
@@ -269,10 +272,12 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
   asm volatile("" : "+v"(tid));
   const int cc = tid % CC, r0 = tid / CC;
   const int col = cc * 8;
-  float bv[8];
+  float bv[8], cen[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[bias_col(col + e)] : 0.0f;
   const bool do_st = ts.stats != nullptr;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cen[e] = do_st && ts.center ? ts.center[col + e] : 0.0f;
   const bool do_cs = ts.colsum != nullptr && ts.gcol0 + col < ts.colsum_cols;
   const bool do_bn = ts.bnb.slab != nullptr;
   float sc[8], sh[8], mu[8], is[8];
@@ -300,8 +305,9 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
     if (do_st) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        t1[e] += v[e];
-        t2[e] += v[e] * v[e];
+        const float d = v[e] - cen[e];
+        t1[e] += d;
+        t2[e] += d * d;
       }
     }
 #pragma unroll

@@ -372,6 +372,13 @@ struct BnFinArgs {
   int training;
   float *mean_o, *invstd_o, *scale_o, *shift_o;
   const float* center;  // non-NULL: s_sum / s_sq are sums of (y - center) and (y - center)^2
+  // shifted first pass (selunet_bn_stats_finalize_shifted): uvar_flag_o = the unbiased variance, or -1
+  // where (mean - center)^2 > flag_ratio * var (its one-pass variance is not exact enough: the
+  // adaptive centered pass re-reads those channels); center_next_o = mean (the next step's center,
+  // may alias center: read before written, per channel)
+  float* uvar_flag_o;
+  float flag_ratio;
+  float* center_next_o;
 };
 
 __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const BnFinArgs& a) {
@@ -389,6 +396,11 @@ __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const B
     mean = (double)a.rmean[c] - b;  // running stats track conv output *with* bias
     var = (double)a.rvar[c];
   }
+  if (a.training && a.uvar_flag_o) {
+    const double d = mean - (a.center ? (double)a.center[c] : 0.0);
+    a.uvar_flag_o[c] = d * d <= (double)a.flag_ratio * var ? (float)(var * (double)a.count / (double)(a.count - 1)) : -1.0f;
+  }
+  if (a.training && a.center_next_o) a.center_next_o[c] = (float)mean;
   const double inv = 1.0 / sqrt(var + (double)a.eps);
   const double sc = (double)a.gamma[c] * inv;
   a.mean_o[c] = (float)mean;
@@ -1480,6 +1492,23 @@ int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, doubl
                      mean, invstd, scale, shift};
   launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
   return check_launch("bn_stats_finalize");
+}
+
+int selunet_bn_stats_finalize_shifted(const float* slab, int64_t rows, double* ws, int64_t count, int32_t c,
+                                      float* center, const float* conv_bias, const float* gamma, const float* beta,
+                                      float ratio, float* mean, float* uvar_flag, float* invstd, float* scale,
+                                      float* shift, void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && center && gamma && beta && mean && uvar_flag && invstd && scale && shift &&
+                      c > 0 && ratio >= 0.0f,
+                  "bn_stats_finalize_shifted: bad arguments");
+  SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
+  BnFinArgs fa{count, conv_bias, gamma, beta, nullptr, nullptr, nullptr, 0.0f, 1e-5f, 1,
+               mean, invstd, scale, shift, center};
+  fa.uvar_flag_o = uvar_flag;
+  fa.flag_ratio = ratio;
+  fa.center_next_o = center;
+  launch_reduce_finalize<2>(slab, rows, c, ws, nullptr, fa, BnbFinArgs{}, as_stream(stream));
+  return check_launch("bn_stats_finalize_shifted");
 }
 
 int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab, int32_t dtype,

@@ -93,8 +93,10 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
 
     Under data parallelism (one process per GPU, `train.py --local_rank ...`) only rank 0 decodes:
     it writes each cache file under a temporary name and renames it into place (os.replace is
-    atomic, so no rank can map a half-written file), all ranks meet at a barrier, and every rank
-    then memory-maps the finished cache — one decoded copy on the host instead of one per GPU."""
+    atomic, so no rank can map a half-written file) while the other ranks poll for the finished
+    files (no collective: a long first decode cannot run into the process group's timeout, and the
+    wait does not go through the GPU backend), and every rank then memory-maps the cache — one
+    decoded copy on the host instead of one per GPU."""
     from PIL import Image
 
     root = os.path.join(data_dir, f"{patch_mag}x_{patch_size}")
@@ -108,11 +110,9 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
     ids = [a.split("_input")[0] for a, _ in pairs]
     shared = cache and parallel.is_initialized() and parallel.world_size() > 1
     if shared and parallel.rank() != 0:
-        torch.distributed.barrier()  # rank 0 has written (or found) the cache
+        _wait_for_files((fi, fl), CACHE_WAIT_S)  # rank 0 writes (or has written) the cache
         return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     if cache and os.path.exists(fi) and os.path.exists(fl):
-        if shared:
-            torch.distributed.barrier()
         return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     imgs = np.empty((len(pairs), patch_size, patch_size, 3), np.uint8)
     labs = np.empty((len(pairs), patch_size, patch_size), np.uint8)
@@ -125,9 +125,21 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
             tmp = f"{path[:-4]}.tmp{os.getpid()}.npy"
             np.save(tmp, arr)
             os.replace(tmp, path)
-    if shared:
-        torch.distributed.barrier()
     return PatchSet(imgs, labs, ids)
+
+
+CACHE_WAIT_S = float(os.environ.get("SELUNET_CACHE_WAIT_S", 6 * 3600))
+
+
+def _wait_for_files(paths, limit_s, poll_s=0.5):
+    """Block until every path exists (they appear atomically, os.replace) or limit_s passes."""
+    import time
+
+    t0 = time.monotonic()
+    while not all(os.path.exists(p) for p in paths):
+        if time.monotonic() - t0 > limit_s:
+            raise TimeoutError(f"rank 0 did not write the patch cache within {limit_s:.0f} s: {paths}")
+        time.sleep(poll_s)
 
 
 # ----------------------------------------------------------------------------- GPU batches

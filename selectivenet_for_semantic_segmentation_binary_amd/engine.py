@@ -137,6 +137,12 @@ class Engine:
         # fp32 training: 3x3 layers on split-fp16 operands (selunet_conv3x3_x2); SELUNET_X2=0 keeps
         # the exact-fp32-MFMA kernels (Winograd / direct)
         self.x2 = dt == torch.float32 and os.environ.get("SELUNET_X2", "1") != "0"
+        # fp32 training BN statistics: the conv epilogue sums y - c with c = the previous step's batch
+        # mean (selunet_epilogue.stats_center), so the one-pass variance is exact enough for almost
+        # every channel after the first step and the centered pass re-reads (almost) nothing;
+        # SELUNET_BN_SHIFT=0 keeps c = 0
+        self.bn_shift = dt == torch.float32 and BN_CENTER_RATIO is not None and \
+            os.environ.get("SELUNET_BN_SHIFT", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -307,13 +313,17 @@ class Engine:
         else:
             g = K.gather(n, h, w, taps, *srcs)
             rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
+        center = None
         if ctx.training:
             stats = K.keep(torch.empty(rows, 2, co, dtype=torch.float32, device=dev))
+            if self.bn_shift:  # (zero when recorded; a replayed step finds the previous step's mean here)
+                center = K.keep(torch.zeros(co, dtype=torch.float32, device=dev))
         if first_x is not None:
-            K.call("selunet_first_conv_fwd", K.ptr(first_x), n, first_x.shape[1], h, w, K.ptr(fwd), K.ptr(y),
-                   K.ptr(stats), self.code, self.stream)
+            K.call("selunet_first_conv_fwd_centered", K.ptr(first_x), n, first_x.shape[1], h, w, K.ptr(fwd),
+                   K.ptr(y), K.ptr(stats), K.ptr(center), self.code, self.stream)
         else:
             ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
+            ep.stats_center = K.ptr(center)
             self._conv3x3(g, fwd, co, kpad, ep, wp.mode, srcs)
         mean, invstd, scale, shift = (K.keep(torch.empty(co, dtype=torch.float32, device=dev)) for _ in range(4))
         if ctx.training and self.dt == torch.float32:
@@ -324,15 +334,22 @@ class Engine:
             # are re-read — where E[y^2] - mean^2 loses digits; SELUNET_BN_TWOPASS=1 re-reads all)
             ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
             uvar = K.keep(torch.zeros(co, dtype=torch.float32, device=dev)) if BN_CENTER_RATIO is not None else None
-            K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
-                   K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
-                   None, K.ptr(uvar), None, 1.0 if uvar is not None else BN_MOMENTUM, BN_EPS, K.ptr(mean),
-                   K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+            if center is not None:  # shifted sums: mean, the one-pass variance or -1 where it is not exact enough
+                K.call("selunet_bn_stats_finalize_shifted", K.ptr(stats), rows, K.ptr(ws), M, co, K.ptr(center),
+                       K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+                       BN_CENTER_RATIO, K.ptr(mean), K.ptr(uvar), K.ptr(invstd), K.ptr(scale), K.ptr(shift),
+                       self.stream)
+            else:
+                K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
+                       K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+                       None, K.ptr(uvar), None, 1.0 if uvar is not None else BN_MOMENTUM, BN_EPS, K.ptr(mean),
+                       K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
             rows2 = K.query("selunet_channel_slab_rows", M)
             slab2 = K.keep(torch.empty(rows2, 2, co, dtype=torch.float32, device=dev))
-            if uvar is not None:
+            if uvar is not None:  # (shifted: the flags decide, ratio +inf)
                 K.call("selunet_bn_centered_partials_adaptive", K.ptr(y), M, co, K.ptr(mean), K.ptr(uvar),
-                       BN_CENTER_RATIO, K.ptr(slab2), self.code, self.stream)
+                       float("inf") if center is not None else BN_CENTER_RATIO, K.ptr(slab2), self.code,
+                       self.stream)
             else:
                 K.call("selunet_bn_centered_partials", K.ptr(y), M, co, K.ptr(mean), K.ptr(slab2), self.code,
                        self.stream)
@@ -354,7 +371,10 @@ class Engine:
                    K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, 0,
                    K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
         st = BNState(y, mean, invstd, scale, shift, n, h, w, co)
-        if ctx.x2:  # range word of relu(bn(y)) for the split-fp16 consumers (batch statistics)
+        # range word of relu(bn(y)) for the split-fp16 consumers. The Samuelson bound |xhat| <= sqrt(M - 1)
+        # holds for statistics over THIS rank's M values (per-rank BatchNorm, DataParallel replica
+        # semantics); a synchronized BatchNorm would need M = the global count here.
+        if ctx.x2:
             st.amax = self._word(ctx, "act:" + name)
             K.call("selunet_act_bound", K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]), co, M,
                    K.ptr(st.amax), self.stream)

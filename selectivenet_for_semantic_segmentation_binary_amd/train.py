@@ -89,7 +89,9 @@ def _free_port():
 
 def spawn(argv, gpu_ids, command=None):
     """One child process per listed GPU id (replaces torch.nn.DataParallel(device_ids=rank),
-    train.py:131-134). The parent never touches the GPU; it waits and returns the worst exit code.
+    train.py:131-134). The parent never touches the GPU; it waits and returns the exit code of the
+    first child that failed on its own (the siblings it then terminates exit with -SIGTERM, which is
+    not reported).
     command: the child command line (default: this module with `argv`)."""
     port = str(_free_port())
     procs = []
@@ -99,6 +101,7 @@ def spawn(argv, gpu_ids, command=None):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port, SELUNET_GPU_ID=str(gid))
         procs.append(subprocess.Popen(cmd, env=env))
     rc = 0
+    terminated = set()  # children this function stopped: their -SIGTERM is not the job's failure
     try:
         # poll every child: the first non-zero exit (of any rank, not just the next one in order)
         # ends the job at once instead of leaving the others blocked in a collective until the
@@ -110,9 +113,11 @@ def spawn(argv, gpu_ids, command=None):
                 if code is None:
                     continue
                 live.remove(p)
-                rc = max(rc, code) if code >= 0 else max(rc, 128 - code)
+                if code != 0 and p.pid not in terminated and rc == 0:
+                    rc = code if code > 0 else 128 - code
                 if code != 0:
                     for q in live:
+                        terminated.add(q.pid)
                         q.terminate()
             time.sleep(0.2)
     finally:

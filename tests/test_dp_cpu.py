@@ -207,3 +207,27 @@ def test_grad_bucketer_overlapped_allreduce():
         err, before_last, nb = out[r]
         assert err < 1e-5
         assert before_last == nb - 1
+
+
+def _cache_worker(rank, world, port, root, out):
+    _init(rank, world, port)
+    from selectivenet_for_semantic_segmentation_binary_amd import data as D
+
+    tr, _ = D.construct_train_valid(root, test_fold=5)
+    ps = D.decode_patch_list(root, tr, patch_mag=200, patch_size=32, cache=True)
+    np.save(os.path.join(out, f"img{rank}.npy"), np.asarray(ps.images))
+    dist.destroy_process_group()
+    parallel.disable()
+
+
+def test_patch_cache_shared_by_ranks_without_a_collective(tmp_path):
+    """data.decode_patch_list under data parallelism (world 2, gloo): rank 0 decodes and writes the
+    uint8 cache, rank 1 waits for the atomically renamed files (no barrier) and maps the same data."""
+    from tests._patchdir import make_patch_dir
+
+    root = make_patch_dir(str(tmp_path / "patches"))
+    out = tmp_path / "out"
+    out.mkdir()
+    _spawn(_cache_worker, 2, root, str(out))
+    a, b = np.load(out / "img0.npy"), np.load(out / "img1.npy")
+    assert a.shape[0] > 0 and np.array_equal(a, b)

@@ -61,14 +61,29 @@ def test_replayed_steps_match_recorded_steps():
         assert np.abs(p_on[k] - p_off[k]).max() <= 5e-3, k
 
 
-def test_replay_with_frozen_weights_is_bit_exact():
+def test_replay_with_frozen_weights_is_bit_exact(monkeypatch):
     # lr=0: parameters never move, the batch repeats, so step 0 (recorded) and steps 1-2
-    # (replayed) run the same forward on the same inputs and must agree bit for bit.
+    # (replayed) run the same forward on the same inputs and must agree bit for bit — with the BN
+    # statistics unshifted (SELUNET_BN_SHIFT=0: the shifted sums of the default depend on the previous
+    # step's mean, test_replay_with_bn_shift_matches_to_rounding)
+    monkeypatch.setenv("SELUNET_BN_SHIFT", "0")
     l_on, o_on, _, net = _run(True, lr=0.0, same_batch=True)
     assert all(e.plan is not None for v in net._engine()._plans.values() for e in v)
     for o in o_on[1:]:
         assert np.array_equal(o, o_on[0])
     assert l_on[1] == l_on[0] and l_on[2] == l_on[0]
+
+
+def test_replay_with_bn_shift_matches_to_rounding():
+    """The default fp32 BN statistics (engine.Engine.bn_shift): the conv epilogue sums y - c with c =
+    the previous step's batch mean. With frozen weights and a repeated batch, steps 1-2 (c = the mean
+    step 0 found) must reproduce step 0 (c = 0) to the rounding of the statistics: outputs within
+    1e-5 relative to the tensor max, loss within 1e-6 relative."""
+    l_on, o_on, _, net = _run(True, lr=0.0, same_batch=True)
+    assert net._engine().bn_shift
+    for o in o_on[1:]:
+        assert np.abs(o - o_on[0]).max() <= 1e-5 * max(1.0, np.abs(o_on[0]).max())
+    assert np.allclose(l_on, l_on[0], rtol=1e-6, atol=0), l_on
 
 
 def test_dropped_graph_releases_plan_and_eval_forward_replays():

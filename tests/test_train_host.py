@@ -157,3 +157,15 @@ def test_decode_patch_list_cache_is_written_atomically(tmp_path):
     b = D.decode_patch_list(str(tmp_path), pairs, 200, 16)
     assert isinstance(b.images, np.memmap) and np.array_equal(np.asarray(b.images), a.images)
     assert np.array_equal(np.asarray(b.labels), a.labels)
+
+
+def test_spawn_reports_the_failing_rank_not_the_terminated_siblings():
+    """train.spawn (one process per --local_rank id): rank 1 fails with code 3 while rank 0 would run
+    for minutes; spawn stops rank 0 and returns 3 (not rank 0's -SIGTERM)."""
+    import sys
+
+    from selectivenet_for_semantic_segmentation_binary_amd.train import spawn
+
+    code = ("import os, sys, time\n"
+            "sys.exit(3) if os.environ['RANK'] == '1' else time.sleep(120)\n")
+    assert spawn([], [0, 1], command=[sys.executable, "-c", code]) == 3
