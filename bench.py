@@ -95,7 +95,7 @@ class KernelTimer:
     MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
             "selunet_conv3x3_wgrad_x2", "selunet_gemm_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
-    HBM = ("selunet_first_conv_fwd", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
+    HBM = ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
            "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
 
@@ -174,7 +174,7 @@ class KernelTimer:
                 flops *= 2.0 / 3.0
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             return kname, "mfma", flops, nbytes, f"wgrad {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
-        if name == "selunet_first_conv_fwd":  # (x, n, cin, h, w, wpack, y, stats, dtype, stream)
+        if name in ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered"):  # (x, n, cin, h, w, wpack, y, ...)
             n, cin, h, w = (_i(a) for a in args[1:5])
             m = n * h * w
             return (f"first_conv_fwd<{t}>", "hbm", 2.0 * m * 64 * 9 * cin, m * cin * 4 + m * 64 * esz,

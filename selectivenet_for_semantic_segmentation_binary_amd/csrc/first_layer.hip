@@ -32,19 +32,18 @@ __device__ __forceinline__ void tile_coords(unsigned t, int tiles_x, int tiles_y
 }
 
 template <typename T>
-__global__ void __launch_bounds__(FTHREADS, 2)
+__global__ void __launch_bounds__(FTHREADS, 3)
 first_conv_fwd_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ wp, EpiArg ep,
                       int tiles_x, int tiles_y, int total_tiles) {
   constexpr int RB = FK * (int)sizeof(T) + 16;  // LDS row bytes (conflict-free 16-row fragment reads)
   constexpr int XR = (3 * FH * FH + FTHREADS - 1) / FTHREADS;  // halo values per thread
-  // [ A rows + input halo | epilogue tile (aliases them) ][ weights, staged once ]
-  constexpr int SMEM_MAIN = FPIX * RB + 3 * FH * FH * 4;
-  constexpr int SMEM_EPI = FPIX * (FCO + 4) * 4;
-  constexpr int SMEM_T = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_T + FCO * RB];
+  // [ A rows | input halo | weights, staged once | per-wave statistics ]: 50 KB, three workgroups per
+  // CU (the accumulators are stored straight from registers: no LDS epilogue tile)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[FPIX * RB + 3 * FH * FH * 4 + FCO * RB];
+  __shared__ float red[4][2][FCO];
   unsigned char* As = smem;
   float* Xs = reinterpret_cast<float*>(smem + FPIX * RB);
-  unsigned char* Bs = smem + SMEM_T;
+  unsigned char* Bs = smem + FPIX * RB + 3 * FH * FH * 4;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
@@ -69,17 +68,22 @@ first_conv_fwd_kernel(const float* __restrict__ x, int cin, int h, int w, const 
     return hv;
   };
   constexpr int WV = FK * (int)sizeof(T) / 16;  // 16-B vectors per weight row
-  auto stage_weights = [&]() __attribute__((always_inline)) {
-    for (int i = tid; i < FCO * WV; i += FTHREADS) {
-      const int row = i / WV, v = i - row * WV;
-      *reinterpret_cast<uint4*>(Bs + row * RB + v * 16) =
-          *reinterpret_cast<const uint4*>(wp + row * FK + v * (16 / sizeof(T)));
-    }
-  };
+  for (int i = tid; i < FCO * WV; i += FTHREADS) {
+    const int row = i / WV, v = i - row * WV;
+    *reinterpret_cast<uint4*>(Bs + row * RB + v * 16) =
+        *reinterpret_cast<const uint4*>(wp + row * FK + v * (16 / sizeof(T)));
+  }
+  // this lane's two output columns (32x32 C layout: column lane & 31 of subtile b), their bias and
+  // statistics shift
+  float bias[2], cen[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    bias[b] = ep.bias ? ep.bias[b * 32 + l32] : 0.0f;
+    cen[b] = ep.stats_center ? ep.stats_center[b * 32 + l32] : 0.0f;
+  }
 
   int t = (int)b0;
   Halo cur = load_halo(t < total_tiles ? t : 0);
-  stage_weights();
   for (; t < total_tiles; t += gridDim.x) {
     int img, y0, x0;
     tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
@@ -134,19 +138,45 @@ first_conv_fwd_kernel(const float* __restrict__ x, int cin, int h, int w, const 
 #pragma unroll
         for (int b = 0; b < 2; ++b) Mma<T>::run(acc[a][b], af[a], bfr[b]);
     }
-    __syncthreads();
 
-    float* tile = reinterpret_cast<float*>(smem);
-    acc_to_lds<2, 2, FCO>(tile, acc, wave * 64, 0, lane);
-    __syncthreads();
-    auto dst = [&](int pix, int c) -> T* {
-      const int y = y0 + pix / FT, xx = x0 + pix % FT;
-      if (y >= h || xx >= w) return nullptr;
-      return reinterpret_cast<T*>(ep.out0) + (((int64_t)img * h + y) * w + xx) * FCO + c;
-    };
-    auto bias_col = [&](int c) { return c; };
-    lds_tile_store<T, FPIX, FCO, FTHREADS>(tile, tid, dst, ep.bias, bias_col, tile_stats(ep, t, 0, FCO));
-    __syncthreads();  // the tile LDS is restaged by the next iteration
+    // epilogue from registers: y (+ bias) at pixel (wave*64 + a*32 + row, column b*32 + l32) — one
+    // accumulator register is two 128-B runs (fp32) — and the tile's column statistics of the values
+    // before the bias (shifted by stats_center), summed over the lane's rows, its partner half-wave's
+    // and the four waves
+    float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pix = wave * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const int y = y0 + pix / FT, xx = x0 + pix % FT;
+        if (y >= h || xx >= w) continue;
+        T* dst = reinterpret_cast<T*>(ep.out0) + (((int64_t)img * h + y) * w + xx) * FCO;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float v = acc[a][b][r];
+          dst[b * 32 + l32] = from_f<T>(v + bias[b]);
+          const float d = v - cen[b];
+          t1[b] += d;
+          t2[b] += d * d;
+        }
+      }
+    if (ep.stats) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        t1[b] += __shfl_xor(t1[b], 32, 64);
+        t2[b] += __shfl_xor(t2[b], 32, 64);
+        if (half == 0) {
+          red[wave][0][b * 32 + l32] = t1[b];
+          red[wave][1][b * 32 + l32] = t2[b];
+        }
+      }
+    }
+    __syncthreads();  // statistics in LDS; A rows / halo free for the next tile
+    if (ep.stats && tid < 2 * FCO) {
+      const int s2 = tid / FCO, c = tid - s2 * FCO;
+      ep.stats[((int64_t)t * 2 + s2) * FCO + c] = red[0][s2][c] + red[1][s2][c] + red[2][s2][c] + red[3][s2][c];
+    }
   }
 }
 
@@ -155,69 +185,89 @@ template <typename T>
 __global__ void __launch_bounds__(FTHREADS, 2)
 first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ dy, float* slab,
                         int tiles_x, int tiles_y, int total_tiles, int tiles_per_block) {
-  constexpr int PB = FPIX * (int)sizeof(T) + 16;  // transposed row bytes (256 pixels + pad)
+  // a tile runs as two stages of HP = 128 pixels (tile rows 0-7, 8-15): 54 KB of LDS, two workgroups
+  // per CU (a whole-tile stage needed 104 KB: one workgroup, every phase exposed)
+  constexpr int HP = FPIX / 2;
+  constexpr int PB = HP * (int)sizeof(T) + 16;  // transposed row bytes (128 pixels + pad)
   constexpr int E = 16 / (int)sizeof(T);
-  constexpr int DV = FCO / E;                      // 16-B vectors per dY pixel row
+  constexpr int CH = FCO / 2;                    // dY channels per thread: two threads per pixel
+  constexpr int DV = CH / E;                     // 16-B vectors per thread and stage
+  constexpr int XR = (3 * FH * FH + FTHREADS - 1) / FTHREADS;
   __shared__ __attribute__((aligned(16))) unsigned char smem[FCO * PB + FK * PB + 3 * FH * FH * 4];
-  unsigned char* Ds = smem;                        // [64 co][256 px]
-  unsigned char* Cs = smem + FCO * PB;             // [32 k][256 px]
+  unsigned char* Ds = smem;                        // [64 co][128 px]
+  unsigned char* Cs = smem + FCO * PB;             // [32 k][128 px]
   float* Xs = reinterpret_cast<float*>(Cs + FK * PB);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
-  const int wa = wave & 1, wp = wave >> 1;  // co subtile, pixel half
+  const int wa = wave & 1, wp = wave >> 1;  // co subtile, 64-pixel half of the stage
+  const int sp = tid % HP, hc = tid / HP;   // staging: stage pixel, channel (dY) / k (columns) half
   const int tb = blockIdx.x * tiles_per_block;
   const int te = min(total_tiles, tb + tiles_per_block);
 
   struct Loaded {
     uint4 d[DV];
-    float xh[(3 * FH * FH + FTHREADS - 1) / FTHREADS];
+    float xh[XR];
   };
-  auto load = [&](int t) __attribute__((always_inline)) {
+  // job j = (tile tb + j / 2, stage j % 2): this thread's dY channels of its pixel, and at stage 0
+  // the tile's input halo
+  auto load = [&](int j) __attribute__((always_inline)) {
     Loaded L;
+    const int t = tb + (j >> 1), st = j & 1;
     int img, y0, x0;
     tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
-    const int y = min(y0 + tid / FT, h - 1), xx = min(x0 + tid % FT, w - 1);
-    const T* src = dy + (((int64_t)img * h + y) * w + xx) * FCO;
+    const int pix = st * HP + sp;
+    const int y = min(y0 + pix / FT, h - 1), xx = min(x0 + pix % FT, w - 1);
+    const T* src = dy + (((int64_t)img * h + y) * w + xx) * FCO + hc * CH;
 #pragma unroll
     for (int v = 0; v < DV; ++v) L.d[v] = *reinterpret_cast<const uint4*>(src + v * E);
+    if (st == 0) {
 #pragma unroll
-    for (int r = 0; r < (3 * FH * FH + FTHREADS - 1) / FTHREADS; ++r) {
-      const int i = min(r * FTHREADS + tid, cin * FH * FH - 1);
-      const int c = i / (FH * FH), rr = i - c * (FH * FH);
-      const int ys = min(max(y0 - 1 + rr / FH, 0), h - 1), xs = min(max(x0 - 1 + rr % FH, 0), w - 1);
-      L.xh[r] = x[(((int64_t)img * cin + c) * h + ys) * w + xs];
+      for (int r = 0; r < XR; ++r) {
+        const int i = min(r * FTHREADS + tid, cin * FH * FH - 1);
+        const int c = i / (FH * FH), rr = i - c * (FH * FH);
+        const int ys = min(max(y0 - 1 + rr / FH, 0), h - 1), xs = min(max(x0 - 1 + rr % FH, 0), w - 1);
+        L.xh[r] = x[(((int64_t)img * cin + c) * h + ys) * w + xs];
+      }
     }
     return L;
   };
-  auto stage = [&](const Loaded& L, int t) __attribute__((always_inline)) {
+  auto stage = [&](const Loaded& L, int j) __attribute__((always_inline)) {
+    const int t = tb + (j >> 1), st = j & 1;
     int img, y0, x0;
     tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
+    if (st == 0) {
 #pragma unroll
-    for (int r = 0; r < (3 * FH * FH + FTHREADS - 1) / FTHREADS; ++r) {
-      const int i = r * FTHREADS + tid;
-      if (i < cin * FH * FH) {
-        const int c = i / (FH * FH), rr = i - c * (FH * FH);
-        const int ys = y0 - 1 + rr / FH, xs = x0 - 1 + rr % FH;
-        Xs[i] = ((unsigned)ys < (unsigned)h && (unsigned)xs < (unsigned)w) ? L.xh[r] : 0.0f;
+      for (int r = 0; r < XR; ++r) {
+        const int i = r * FTHREADS + tid;
+        if (i < cin * FH * FH) {
+          const int c = i / (FH * FH), rr = i - c * (FH * FH);
+          const int ys = y0 - 1 + rr / FH, xs = x0 - 1 + rr % FH;
+          Xs[i] = ((unsigned)ys < (unsigned)h && (unsigned)xs < (unsigned)w) ? L.xh[r] : 0.0f;
+        }
       }
     }
-    // dY row of pixel tid, transposed (a pixel outside the image contributes nothing)
-    const bool inside = y0 + tid / FT < h && x0 + tid % FT < w;
-    T* dcol = reinterpret_cast<T*>(Ds) + tid;
+    // this thread's dY channels of stage pixel sp, transposed (a pixel outside the image contributes
+    // nothing)
+    const int pix = st * HP + sp;
+    const bool inside = y0 + pix / FT < h && x0 + pix % FT < w;
+    T* dcol = reinterpret_cast<T*>(Ds) + sp;
 #pragma unroll
     for (int v = 0; v < DV; ++v) {
       T e[E];
       __builtin_memcpy(e, &L.d[v], 16);
 #pragma unroll
-      for (int j = 0; j < E; ++j) dcol[(v * E + j) * (PB / (int)sizeof(T))] = inside ? e[j] : from_f<T>(0.0f);
+      for (int q = 0; q < E; ++q) dcol[(hc * CH + v * E + q) * (PB / (int)sizeof(T))] = inside ? e[q] : from_f<T>(0.0f);
     }
   };
-  auto build_cols = [&]() __attribute__((always_inline)) {
-    const int py = tid / FT, px = tid % FT;
-    T* ccol = reinterpret_cast<T*>(Cs) + tid;
+  // im2col columns k = 16 hc .. 16 hc + 15 of stage pixel sp
+  auto build_cols = [&](int st) __attribute__((always_inline)) {
+    const int pix = st * HP + sp;
+    const int py = pix / FT, px = pix % FT;
+    T* ccol = reinterpret_cast<T*>(Cs) + sp;
 #pragma unroll
-    for (int k = 0; k < FK; ++k) {
+    for (int kk = 0; kk < FK / 2; ++kk) {
+      const int k = hc * (FK / 2) + kk;
       float v = 0.0f;
       if (k < 9 * cin) {
         const int tap = k / cin, c = k - tap * cin;
@@ -228,23 +278,24 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
   };
 
   f32x16 acc = f32x16{};
-  if (tb < te) {
-    Loaded cur = load(tb);
-    for (int t = tb; t < te; ++t) {
-      stage(cur, t);
+  const int jobs = 2 * (te - tb);
+  if (jobs > 0) {
+    Loaded cur = load(0);
+    for (int j = 0; j < jobs; ++j) {
+      stage(cur, j);
       __syncthreads();  // Xs, Ds written
-      build_cols();
-      if (t + 1 < te) cur = load(t + 1);
+      build_cols(j & 1);
+      if (j + 1 < jobs) cur = load(j + 1);
       __syncthreads();  // Cs written
-      // out[co][k] += sum over this wave's 128 pixels
+      // out[co][k] += sum over this wave's 64 pixels of the stage
 #pragma unroll
-      for (int q = 0; q < 128 * (int)sizeof(T) / 32; ++q) {
-        const int boff = wp * 128 * (int)sizeof(T) + q * 32 + half * 16;
+      for (int q = 0; q < 64 * (int)sizeof(T) / 32; ++q) {
+        const int boff = wp * 64 * (int)sizeof(T) + q * 32 + half * 16;
         const uint4 af = *reinterpret_cast<const uint4*>(Ds + (wa * 32 + l32) * PB + boff);
         const uint4 bfr = *reinterpret_cast<const uint4*>(Cs + l32 * PB + boff);
         Mma<T>::run(acc, af, bfr);
       }
-      __syncthreads();  // before the next tile overwrites Ds / Cs / Xs
+      __syncthreads();  // before the next job overwrites Ds / Cs / Xs
     }
   }
   // combine the two pixel halves, write this block's [64][32] partial sums
@@ -285,7 +336,7 @@ extern "C" int selunet_first_conv_fwd_centered(const float* x, int32_t n, int32_
   SELUNET_REQUIRE(center == nullptr || stats != nullptr, "first_conv_fwd: center only with stats");
   EpiArg ep{y, nullptr, nullptr, stats, SELUNET_EP_PLAIN, 0, nullptr,
             BnBwdArg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}, nullptr, center};
-  const unsigned blocks = (unsigned)std::min(tiles, 2048);  // 8 tiles in flight per CU pair of workgroups
+  const unsigned blocks = (unsigned)std::min(tiles, 3072);  // (three resident workgroups per CU)
   if (dtype == SELUNET_F32)
     hipLaunchKernelGGL(first_conv_fwd_kernel<float>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h, w,
                        reinterpret_cast<const float*>(wpack), ep, tx, ty, tiles);
