@@ -237,7 +237,7 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * required, dgrad optional), ConvTranspose2d entries as selunet_pack_convT (w [ci][co][2][2]).
  * `offset` is computed by the call. Replaces the per-tensor loop over model.py's conv/unpool
  * parameters (model.py:11,44,51,57) that casting fp32 masters to the compute operands needs. */
-#define SELUNET_PACK_MAX 24
+#define SELUNET_PACK_MAX 32
 /* SELUNET_PACK_CONV3X3_WINO (fp32): fwd = [co][12*ci] and dgrad = [ci][12*co] Winograd weight
  * operands of selunet_conv3x3_wino (k_pad = 12*ci; dgrad from the flipped/transposed kernel). */
 /* SELUNET_PACK_CONV3X3_X2 (fp32): split-fp16 operands of selunet_conv3x3_x2, k_pad = 9*ci; fwd =
@@ -247,12 +247,16 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * matrix: fwd + co*9*ci (co floats), dgrad + ci*9*co (ci floats). ci, co multiples of 32. */
 /* SELUNET_PACK_CONVT_X2 (fp32): the same split-fp16 format for a ConvTranspose2d weight [ci][co][2][2]:
  * fwd = [4*co][ci] (row (a*2+b)*co + o, k_pad = ci) + 4*co unscale factors, dgrad = [ci][4*co] + ci. */
+/* SELUNET_PACK_COPY (any dtype): co*ci fp32 values w -> fwd unchanged (dgrad unused) — the heads'
+ * current weights and biases (model.py:62,65,66) gathered into the contiguous [heads][64] / [heads]
+ * operands of selunet_heads_fwd in the same launch. */
 enum {
   SELUNET_PACK_CONV3X3 = 0,
   SELUNET_PACK_CONVT = 1,
   SELUNET_PACK_CONV3X3_WINO = 2,
   SELUNET_PACK_CONV3X3_X2 = 3,
-  SELUNET_PACK_CONVT_X2 = 4
+  SELUNET_PACK_CONVT_X2 = 4,
+  SELUNET_PACK_COPY = 5
 };
 typedef struct selunet_pack_desc {
   const float* w;
@@ -343,6 +347,16 @@ int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* 
                                        float* running_mean, float* running_var, int64_t* num_batches,
                                        float momentum, float eps, float* mean, float* invstd,
                                        float* scale, float* shift, void* stream);
+/* selunet_bn_stats_finalize_centered that also folds the split-fp16 range word of relu(bn(y)) into
+ * *bound (zeroed by the caller before the step): atomic max over the channels of
+ * (|gamma_c| * sqrt(count) + |beta_c|) * 1.0001 — the per-channel form of selunet_act_bound's
+ * Samuelson bound (never larger), without its separate launch. bound may be NULL. */
+int selunet_bn_stats_finalize_centered_bound(const float* slab, int64_t rows, double* ws, double* sums,
+                                             int64_t count, int32_t c, const float* center,
+                                             const float* conv_bias, const float* gamma, const float* beta,
+                                             float* running_mean, float* running_var, int64_t* num_batches,
+                                             float momentum, float eps, float* mean, float* invstd,
+                                             float* scale, float* shift, float* bound, void* stream);
 int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums,
                                   int64_t count, int32_t c, const float* gamma, const float* invstd,
                                   float* dgamma, float* dbeta, float* dbias, float* coef,

@@ -49,7 +49,7 @@ class PackDesc(ctypes.Structure):
                 ("ci", c_int32), ("k_pad", c_int32), ("offset", c_int64)]
 
 
-PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2, PACK_CONVT_X2 = 24, 0, 1, 2, 3, 4
+PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2, PACK_CONVT_X2, PACK_COPY = 32, 0, 1, 2, 3, 4, 5
 WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
 
 
@@ -120,6 +120,8 @@ SIGNATURES = {
     "selunet_bn_centered_partials_adaptive": (c_int32, [P, c_int64, c_int32, P, P, c_float, P, c_int32, P]),
     "selunet_bn_stats_finalize_centered": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P,
                                                      c_float, c_float, P, P, P, P, P]),
+    "selunet_bn_stats_finalize_centered_bound": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P,
+                                                           c_float, c_float, P, P, P, P, P, P]),
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_amax": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, P, c_int32, P]),

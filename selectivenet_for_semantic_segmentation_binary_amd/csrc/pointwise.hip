@@ -141,6 +141,8 @@ __global__ void pack_weights_kernel(selunet_pack_list l, int64_t total) {
       const double g0 = fw ? gw[0] : gw[2], g1 = gw[1], g2 = fw ? gw[2] : gw[0];
       const double u = xi == 0 ? g0 : xi == 1 ? 0.5 * (g0 + g1 + g2) : xi == 2 ? 0.5 * (g0 - g1 + g2) : g2;
       (fw ? fwd : dg)[q] = from_f<T>((float)u);
+    } else if (d.kind == SELUNET_PACK_COPY) {  // fp32 values unchanged
+      reinterpret_cast<float*>(d.fwd)[j] = w[j];
     } else {  // as pack_convT_kernel: w[c][o][ab]
       const int ci = d.ci, co = d.co;
       const int ab = (int)(j & 3);
@@ -379,6 +381,10 @@ struct BnFinArgs {
   float* uvar_flag_o;
   float flag_ratio;
   float* center_next_o;
+  // bound_o (selunet_bn_stats_finalize_centered_bound): atomic max of (|gamma_c| * bound_sq + |beta_c|)
+  // over the channels, the split-fp16 range word of relu(bn(y)) (see selunet_act_bound)
+  float* bound_o;
+  float bound_sq;
 };
 
 __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const BnFinArgs& a) {
@@ -516,8 +522,12 @@ __global__ void __launch_bounds__(1024) reduce_finalize_kernel(const S* __restri
     t[s] = x;
     if (sums_out) sums_out[s * C + c] = x;
   }
-  if constexpr (SETS == 2) bn_finalize_one(c, t[0], t[1], fa);
-  else bn_bwd_finalize_one(c, C, t[0], t[1], t[2], ba);
+  if constexpr (SETS == 2) {
+    bn_finalize_one(c, t[0], t[1], fa);
+    if (fa.bound_o) atomic_amax(fa.bound_o, (fabsf(fa.gamma[c]) * fa.bound_sq + fabsf(fa.beta[c])) * 1.0001f);
+  } else {
+    bn_bwd_finalize_one(c, C, t[0], t[1], t[2], ba);
+  }
 }
 
 // rows up to which the fused reductions read the fp32 slab in one launch; above it a first level
@@ -1343,6 +1353,9 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
       SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == 12 * d.ci,
                       "pack_weights: Winograd entry %d needs fp32, fwd and k_pad = 12*ci", t);
       off += (int64_t)d.co * 12 * d.ci + (d.dgrad ? (int64_t)d.ci * 12 * d.co : 0);
+    } else if (d.kind == SELUNET_PACK_COPY) {
+      SELUNET_REQUIRE(d.fwd && !d.dgrad, "pack_weights: copy entry %d needs fwd only", t);
+      off += (int64_t)d.co * d.ci;
     } else {
       SELUNET_REQUIRE(d.kind == SELUNET_PACK_CONVT, "pack_weights: bad kind in entry %d", t);
       off += (int64_t)d.ci * d.co * 4;
@@ -1528,18 +1541,31 @@ int selunet_bn_centered_partials_adaptive(const void* y, int64_t m, int32_t c, c
   return check_launch("bn_centered_partials_adaptive");
 }
 
+int selunet_bn_stats_finalize_centered_bound(const float* slab, int64_t rows, double* ws, double* sums,
+                                             int64_t count, int32_t c, const float* center, const float* conv_bias,
+                                             const float* gamma, const float* beta, float* running_mean,
+                                             float* running_var, int64_t* num_batches, float momentum, float eps,
+                                             float* mean, float* invstd, float* scale, float* shift, float* bound,
+                                             void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && center && gamma && beta && mean && invstd && scale && shift && c > 0,
+                  "bn_stats_finalize_centered: bad arguments");
+  SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
+  BnFinArgs fa{count, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, 1,
+               mean, invstd, scale, shift, center};
+  fa.bound_o = bound;
+  fa.bound_sq = (float)std::sqrt((double)count);
+  launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
+  return check_launch("bn_stats_finalize_centered");
+}
+
 int selunet_bn_stats_finalize_centered(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,
                                        int32_t c, const float* center, const float* conv_bias, const float* gamma,
                                        const float* beta, float* running_mean, float* running_var,
                                        int64_t* num_batches, float momentum, float eps, float* mean, float* invstd,
                                        float* scale, float* shift, void* stream) {
-  SELUNET_REQUIRE(slab && ws && rows > 0 && center && gamma && beta && mean && invstd && scale && shift && c > 0,
-                  "bn_stats_finalize_centered: bad arguments");
-  SELUNET_REQUIRE(count > 1, "Expected more than 1 value per channel when training (got %lld)", (long long)count);
-  const BnFinArgs fa{count, conv_bias, gamma, beta, running_mean, running_var, num_batches, momentum, eps, 1,
-                     mean, invstd, scale, shift, center};
-  launch_reduce_finalize<2>(slab, rows, c, ws, sums, fa, BnbFinArgs{}, as_stream(stream));
-  return check_launch("bn_stats_finalize_centered");
+  return selunet_bn_stats_finalize_centered_bound(slab, rows, ws, sums, count, c, center, conv_bias, gamma, beta,
+                                                  running_mean, running_var, num_batches, momentum, eps, mean, invstd,
+                                                  scale, shift, nullptr, stream);
 }
 
 int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,

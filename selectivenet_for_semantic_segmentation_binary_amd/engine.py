@@ -235,9 +235,11 @@ class Engine:
             return False
         return self._shape_ok("selunet_conv3x3_x2_ok", name, ci, co, hw, need_dgrad)
 
-    def pack_weights(self, P, need_dgrad=True, hw=None, training=False):
+    def pack_weights(self, P, need_dgrad=True, hw=None, training=False, heads=()):
         """fp32 master weights -> GEMM operand layouts in the compute dtype (one launch for all);
         fp32 layers at input resolution hw get the split-fp16 (training) or Winograd operands.
+        heads: (name, channels) of the output heads whose weights / biases are gathered, in the same
+        launch, into the contiguous fp32 operands of the heads kernel (packs["heads"] = (w, b)).
         Returns name -> WPack."""
         dev = P["encoder_layer_1_2.0.weight"].device
         packs = {}
@@ -276,6 +278,18 @@ class Engine:
                 pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), K.PACK_CONVT, co, ci, 0, 0)
             pl.n += 1
             packs[name] = WPack(fwd, dg, ci, co, "x2" if x2 else "direct")
+        if heads:
+            no = sum(c for _, c in heads)
+            hw_, hb_ = (K.keep(torch.empty(no, k, dtype=torch.float32, device=dev)) for k in (64, 1))
+            k = 0
+            if pl.n + 2 * len(heads) > K.PACK_MAX:
+                raise ValueError(f"{len(heads)} heads: more weight-pack entries than SELUNET_PACK_MAX")
+            for h, c in heads:
+                for t, dst, n in ((P[f"{h}.weight"], hw_[k:], c * 64), (P[f"{h}.bias"], hb_[k:], c)):
+                    pl.d[pl.n] = K.PackDesc(K.ptr(t), K.ptr(dst), None, K.PACK_COPY, n, 1, 0, 0)
+                    pl.n += 1
+                k += c
+            packs["heads"] = (hw_, hb_.view(no))
         K.call("selunet_pack_weights", pl, self.code, self.stream)
         return packs
 
@@ -353,11 +367,13 @@ class Engine:
             else:
                 K.call("selunet_bn_centered_partials", K.ptr(y), M, co, K.ptr(mean), K.ptr(slab2), self.code,
                        self.stream)
-            K.call("selunet_bn_stats_finalize_centered", K.ptr(slab2), rows2, K.ptr(ws), None, M, co, K.ptr(mean),
-                   K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
+            # (+ the split-fp16 range word of relu(bn(y)) in the same launch, see below)
+            bound = self._word(ctx, "act:" + name) if ctx.x2 else None
+            K.call("selunet_bn_stats_finalize_centered_bound", K.ptr(slab2), rows2, K.ptr(ws), None, M, co,
+                   K.ptr(mean), K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
                    K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
                    K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS,
-                   K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
+                   K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), K.ptr(bound), self.stream)
         elif ctx.training:  # statistics slab -> fp64 column sums -> batch mean/invstd, running stats: one launch
             ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 2 * co) // 8, dtype=torch.float64, device=dev))
             K.call("selunet_bn_stats_finalize", K.ptr(stats), rows, K.ptr(ws), None, M, co,
@@ -374,10 +390,12 @@ class Engine:
         # range word of relu(bn(y)) for the split-fp16 consumers. The Samuelson bound |xhat| <= sqrt(M - 1)
         # holds for statistics over THIS rank's M values (per-rank BatchNorm, DataParallel replica
         # semantics); a synchronized BatchNorm would need M = the global count here.
+        # (fp32 training folds it into the centered finalize: max_c |gamma_c| sqrt(M) + |beta_c|)
         if ctx.x2:
             st.amax = self._word(ctx, "act:" + name)
-            K.call("selunet_act_bound", K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]), co, M,
-                   K.ptr(st.amax), self.stream)
+            if not (ctx.training and self.dt == torch.float32):
+                K.call("selunet_act_bound", K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]), co, M,
+                       K.ptr(st.amax), self.stream)
         ctx.bn[name] = st
         return st
 
@@ -472,7 +490,14 @@ class Engine:
         n, cin, H, W = x.shape
         ctx = Ctx(self.dt, training, selective, (n, cin, H, W), x=x)
         ctx.ce_heads = ce_heads
-        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W), training=training)
+        heads = LY.HEADS if selective else LY.HEADS[:1]
+        heads = list(ce_heads) if ce_heads is not None else [(h, 1) for h in heads]
+        if sum(c for _, c in heads) > 8:
+            raise ValueError(f"the heads have {sum(c for _, c in heads)} output channels; the MI355X heads kernel "
+                             "takes at most 8")
+        ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W), training=training,
+                                      heads=heads)
+        hw, hb = ctx.wpack.pop("heads")
         ctx.x2 = any(wp.mode == "x2" for wp in ctx.wpack.values())
         if ctx.x2:  # the operand range words of this step, zeroed for their atomic-max producers
             keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy", "du")]
@@ -507,13 +532,7 @@ class Engine:
         d11 = c("decoder_layer_1_1", h1, w1, d12.src())
         M = n * H * W
         if ce_heads is not None:
-            return self._heads_fwd_planes(ctx, P, d11, outs, ce_heads, n, H * W)
-        heads = LY.HEADS if selective else LY.HEADS[:1]
-        hw = K.keep(torch.empty(len(heads), 64, dtype=torch.float32, device=x.device))
-        hb = K.keep(torch.empty(len(heads), dtype=torch.float32, device=x.device))
-        for i, h in enumerate(heads):  # the heads' current weights, gathered in stream order
-            K.call("selunet_memcpy", K.ptr(hw[i]), K.ptr(P[f"{h}.weight"]), 64 * 4, self.stream)
-            K.call("selunet_memcpy", K.ptr(hb[i:]), K.ptr(P[f"{h}.bias"]), 4, self.stream)
+            return self._heads_fwd_planes(ctx, d11, outs, ce_heads, n, H * W, hw, hb)
         o = list(outs) + [None] * (3 - len(outs))
         K.call("selunet_heads_fwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(hw), K.ptr(hb),
                len(heads), K.ptr(o[0]), K.ptr(o[1]), K.ptr(o[2]), self.code, self.stream)
@@ -539,18 +558,8 @@ class Engine:
         d.n, d.hw, d.row_len = k, hw, off
         return d
 
-    def _heads_fwd_planes(self, ctx, P, d11, outs, ce_heads, n, hw):
-        no = sum(c for _, c in ce_heads)
-        if no > 8:
-            raise ValueError(f"the heads have {no} output channels; the MI355X heads kernel takes at most 8")
-        dev = d11.y.device
-        w = K.keep(torch.empty(no, 64, dtype=torch.float32, device=dev))
-        b = K.keep(torch.empty(no, dtype=torch.float32, device=dev))
-        k = 0
-        for h, c in ce_heads:  # the heads' current weights, gathered in stream order
-            K.call("selunet_memcpy", K.ptr(w[k:]), K.ptr(P[f"{h}.weight"]), c * 64 * 4, self.stream)
-            K.call("selunet_memcpy", K.ptr(b[k:]), K.ptr(P[f"{h}.bias"]), c * 4, self.stream)
-            k += c
+    def _heads_fwd_planes(self, ctx, d11, outs, ce_heads, n, hw, w, b):
+        """w [no][64], b [no]: the heads' current weights (gathered by pack_weights)."""
         K.call("selunet_heads_fwd_planes", K.ptr(d11.y), n * hw, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(w), K.ptr(b),
                self._planes(outs, ce_heads, hw), self.code, self.stream)
         ctx.head_w = w
