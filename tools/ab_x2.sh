@@ -1,6 +1,6 @@
 #!/bin/bash
-# x2 conv forward/dgrad timing (tools/conv_bench.py --x2) under the build and every _ab/libselunet_*.so.
-# Run on the GPU box from the repo root; LAYERS / ONLY select.
+# x2 conv forward/dgrad (or ONLY=wgrad: weight gradient) timing (tools/conv_bench.py --x2) under the
+# build and every _ab/libselunet_*.so. Run on the GPU box from the repo root; LAYERS / ONLY select.
 R=$(cd "$(dirname "$0")/.." && pwd)
 for lib in $R/selectivenet_for_semantic_segmentation_binary_amd/libselunet.so $R/_ab/libselunet_*.so; do
   echo "== $(basename $lib)"

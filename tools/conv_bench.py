@@ -89,7 +89,7 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
     return ms, flops / (ms * 1e-3) / 1e12, name, (keep, o0, o1, stats, w)
 
 
-def run_wgrad(n, c_srcs, co, hw, iters, dt=torch.bfloat16):
+def run_wgrad(n, c_srcs, co, hw, iters, dt=torch.bfloat16, x2=False):
     """Weight gradient P^T Q: P = dY [m][co] (1 tap), Q = the layer input gather (9 taps, BN+ReLU of
     the producers), deterministic split partials + reduction (the training default)."""
     dev = "cuda"
@@ -112,7 +112,19 @@ def run_wgrad(n, c_srcs, co, hw, iters, dt=torch.bfloat16):
     ws = torch.empty(max(wsb // 4, 1), device=dev)
     name = K.query("selunet_gemm_kernel_name", ctypes.byref(gp), ctypes.byref(gq), co, 0, code).decode()
 
+    if x2:  # split-fp16 weight gradient straight into the Conv2d layout (range words: timing only)
+        wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", ctypes.byref(gp), ctypes.byref(gq))
+        ws = torch.empty(max(wsb // 4, 1), device=dev)
+        out = torch.empty(co, ci, 3, 3, device=dev)
+        amax = torch.full((1,), 8.0, device=dev)
+        keep.append(amax)
+        name = "conv3x3_wgrad_x2"
+
     def call():
+        if x2:
+            K.call("selunet_conv3x3_wgrad_x2", ctypes.byref(gp), ctypes.byref(gq), K.ptr(ws), wsb, K.ptr(out),
+                   K.ptr(amax), K.ptr(amax), K.ptr(amax), K.stream_ptr())
+            return
         K.call("selunet_gemm_wgrad_ws", ctypes.byref(gp), ctypes.byref(gq), K.ptr(out), K.ptr(ws), wsb, code,
                K.stream_ptr())
 
@@ -152,7 +164,7 @@ def main():
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
         if a.only == "wgrad":
-            ms, tf, kn = run_wgrad(a.batch, (c0, c1), co, hw, a.iters, dt)
+            ms, tf, kn = run_wgrad(a.batch, (c0, c1), co, hw, a.iters, dt, a.x2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
