@@ -553,105 +553,10 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   // (X2 at BN = 128: fp32 statistics registers, as the Winograd kernel — fp64 ones spill)
   using Acc = std::conditional_t<X2 && BN == 128, float, typename StatAcc<T>::type>;
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
-  // REG_EPI (the 16x16x32 form): the epilogue stores from the accumulators and keeps per-lane column
-  // sums (r1..r3, fp64, the lane's AN columns) instead of staging the tile through LDS — the LDS then
-  // never leaves the halo / weight pipeline, so the next tile's first chunk is staged during this
-  // tile's last chunk (no deferred halo write, two barriers fewer per tile): 3 % on the 64-column
-  // layers. (The 32x32 form at BN = 128 spills more with it: 156 B per lane against 36.)
-  constexpr bool REG_EPI = M16;
-  constexpr int EPI_RR = WAVES_M * 4;  // the epilogue's per-column partial rows: (wave row, lane group)
-  static_assert(!REG_EPI || EPI_RR * BN * 3 * (int)sizeof(double) <= (int)sizeof(smem),
-                "register-epilogue statistics scratch exceeds LDS");
-  Acc s1[8] = {}, s2[8] = {}, s3[8] = {};  // (unused under REG_EPI)
-  double r1[REG_EPI ? AN : 1] = {}, r2[REG_EPI ? AN : 1] = {}, r3[REG_EPI ? AN : 1] = {};
+  Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float amx = 0.0f;  // running max |stored value| (epilogue range word)
   const TileStats ts = tile_stats(ep, prow, n0, N);
   float* tile = reinterpret_cast<float*>(smem);  // epilogue: [256][BN + 4] over the whole LDS
-  // REG_EPI epilogue of the tile at (img, y0, x0): unscale, store, statistics; accumulators reset
-  auto reg_epi = [&](int img, int y0, int x0) __attribute__((always_inline)) {
-    if constexpr (REG_EPI) {
-      // 16x16 C layout: acc[a][b][i] is pixel (tile row wm * RT + a, x = 4 (lane >> 4) + i), column
-      // wn * 64 + 16 b + (lane & 15): 16 consecutive columns = 64 B per pixel per store; the
-      // statistics follow lds_tile_store_acc (fp32 over the lane's rows of the tile, fp64 across tiles).
-      int lc = l16;
-      asm volatile("" : "+v"(lc));  // column coefficients reloaded per tile, not pinned through the main loop
-      const bool do_st = ts.stats != nullptr;
-      const bool do_bn = ts.bnb.slab != nullptr;
-      float bv[AN], cen[AN], sc[AN], sh[AN], mu[AN], is[AN];
-      bool cs[AN];
-#pragma unroll
-      for (int b = 0; b < AN; ++b) {
-        const int col = wn * 64 + b * 16 + lc;
-        bv[b] = ep.bias ? ep.bias[n0 + col] : 0.0f;
-        cen[b] = do_st && ts.center ? ts.center[col] : 0.0f;
-        cs[b] = ts.colsum != nullptr && n0 + col < ts.colsum_cols;
-        sc[b] = sh[b] = mu[b] = is[b] = 0.0f;
-        if (do_bn) {
-          sc[b] = ts.bnb.scale[col];
-          sh[b] = ts.bnb.shift[col];
-          mu[b] = ts.bnb.mean[col];
-          is[b] = ts.bnb.invstd[col];
-        }
-      }
-      // the tile's columns lie in one output (SPLIT: split % BN == 0, checked on the host)
-      float* ob = reinterpret_cast<float*>(ep.out0);
-      int ldo = N, oc = n0;
-      if (ep.mode == SELUNET_EP_SPLIT) {
-        if (n0 < ep.split) {
-          ldo = ep.split;
-        } else {
-          ob = reinterpret_cast<float*>(ep.out1);
-          ldo = N - ep.split;
-          oc = n0 - ep.split;
-        }
-      }
-      float t1[AN] = {}, t2[AN] = {}, t3[AN] = {};
-#pragma unroll
-      for (int a = 0; a < RT; ++a) {
-        const int yy = y0 + wm * RT + a;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int xx = x0 + 4 * kg + i;
-          if (yy >= g.h || xx >= g.w) continue;
-          const int64_t m = ((int64_t)img * g.h + yy) * g.w + xx;
-          float* orow = ob + m * ldo + oc + wn * 64 + lc;
-          const float* yrow =
-              do_bn ? reinterpret_cast<const float*>(ts.bnb.y) + m * N + n0 + wn * 64 + lc : nullptr;
-#pragma unroll
-          for (int b = 0; b < AN; ++b) {
-            const float v = acc[a][b][i] * cfac[b];
-            if (do_st) {
-              const float d = v - cen[b];
-              t1[b] += d;
-              t2[b] += d * d;
-            }
-            const float o = v + bv[b];
-            orow[b * 16] = o;
-            if (ts.amax) amx = fmaxf(amx, fabsf(o));
-            if (cs[b]) t1[b] += o;
-            if (do_bn) {
-              const float yv = yrow[b * 16];
-              const float da = yv * sc[b] + sh[b] > 0.0f ? o : 0.0f;
-              const float xh = (yv - mu[b]) * is[b];
-              t1[b] += da;
-              t2[b] += da * xh;
-              t3[b] += xh;
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < AN; ++b) {
-        r1[b] += (double)t1[b];
-        r2[b] += (double)t2[b];
-        r3[b] += (double)t3[b];
-      }
-#pragma unroll
-      for (int a = 0; a < AM; ++a)
-#pragma unroll
-        for (int b = 0; b < AN; ++b) acc[a][b] = AccT{};
-    }
-  };
   uint4 ra[A_ROUNDS];
   int J = 0;  // job (tile, chunk) counter: halo buffer J & 1
   int S = 0;  // step counter: weight buffer S & 1
@@ -662,10 +567,9 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     for (int c = 0; c < nchunks; ++c, ++J) {
       const bool last_c = c + 1 == nchunks;
       const bool has_next = !last_c || i + 1 < ntl;
-      // next job is the next tile: with the LDS-staged epilogue its LDS writes wait for the epilogue
-      const bool defer = !REG_EPI && last_c && has_next;
+      const bool defer = last_c && has_next;  // next job is the next tile: LDS writes after the epilogue
       int nimg = img, ny0 = y0, nx0 = x0;
-      if (last_c && has_next) tile_xy(i + 1, nimg, ny0, nx0);
+      if (defer) tile_xy(i + 1, nimg, ny0, nx0);
       const int nc = !has_next ? c : (last_c ? 0 : c + 1);
       int cs;
       const SrcArg sn = chunk_src(nc, cs);
@@ -724,15 +628,21 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     }
 
     // ------------------------------------------------------------ epilogue of tile i
-    if constexpr (X2 && !REG_EPI) {
+    if constexpr (X2) {
 #pragma unroll
       for (int a = 0; a < AM; ++a)
 #pragma unroll
         for (int b = 0; b < AN; ++b) acc[a][b] *= cfac[b];
     }
-    if constexpr (REG_EPI) {
-      reg_epi(img, y0, x0);
-      continue;  // next tile: its first chunk is already staged
+    if constexpr (M16) {
+      // 16x16 C layout: column lane & 15, rows 4 (lane >> 4) + i of the subtile (tile row py)
+#pragma unroll
+      for (int a = 0; a < RT; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            tile[(wm * WPIX + a * 16 + 4 * kg + i) * (BN + 4) + wn * 64 + b * 16 + l16] = acc[a][b][i];
     } else {
       acc_to_lds<MT, NT, BN>(tile, acc, wm * WPIX, wn * 64, lane);
     }
@@ -765,36 +675,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       __syncthreads();
     }
   }
-  if constexpr (REG_EPI) {
-    // per-lane column sums -> one slab row per workgroup: the (wave row, lane group) partials reduced in
-    // a fixed order through LDS (free: every MFMA of the last tile has read its operands)
-    if (ts.amax) atomic_amax(ts.amax, amx);
-    const bool do_st = ts.stats != nullptr, do_bn = ts.bnb.slab != nullptr;
-    if (do_st || ts.colsum != nullptr || do_bn) {
-      const int nst = do_bn ? 3 : (do_st ? 2 : 1);
-      constexpr int RR = EPI_RR;  // partial rows per column
-      double* red = reinterpret_cast<double*>(smem);
-      __syncthreads();
-#pragma unroll
-      for (int b = 0; b < AN; ++b) {
-        double* q = red + ((wm * 4 + kg) * BN + wn * 64 + b * 16 + l16) * 3;
-        q[0] = r1[b];
-        q[1] = r2[b];
-        q[2] = r3[b];
-      }
-      __syncthreads();
-      for (int e = tid; e < BN * nst; e += HTHREADS) {
-        const int c = e % BN, k = e / BN;
-        double v = 0.0;
-        for (int r = 0; r < RR; ++r) v += red[(r * BN + c) * 3 + k];
-        if (do_bn) ts.bnb.slab[k * ts.ld + c] = (float)v;
-        else if (do_st) ts.stats[k * ts.ld + c] = (float)v;
-        else if (ts.gcol0 + c < ts.colsum_cols) ts.colsum[c] = (float)v;
-      }
-    }
-  } else {
-    tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
-  }
+  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
 }
 
 // =========================================================================== fp32 Winograd F(2,3)
@@ -1285,7 +1166,7 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
       const bool more = pt + 1 < (int)pt_end;
       load_tile(more ? pt + 1 : pt);
       __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
-#pragma unroll
+  #pragma unroll
       for (int ks = 0; ks < WTH; ++ks) {   // one tile row (16 pixels) per k-step
         const int prow = ks * WTW + 8 * half + q4;
         const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
@@ -1306,10 +1187,10 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
           return __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
         };
         bf16x8 bfr[NTAP];
-#pragma unroll
+  #pragma unroll
         for (int t = 0; t < PF && t < NTAP; ++t) bfr[t] = read_tap(t);
         __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * PF, 0);
-#pragma unroll
+  #pragma unroll
         for (int t = 0; t < NTAP; ++t) {
           if (t < NTP) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[t], acc[t], 0, 0, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -2344,15 +2225,13 @@ static void launch_x2(const GatherArg& g, const float* w, int N, const EpiArg& e
   const int k_pad = 9 * g.Ctot;
   // 16x16x32 MFMAs at BN = 64 (1-4 % faster per layer); at BN = 128 they cost 20-25 % (the extra
   // fragment registers spill: 180 B of scratch per lane against 44) — DESIGN.md §3
-  hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true, BN == 64>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, w, N, k_pad, ep, n_tiles, tiles_x,
-                     tiles_y, (int)conv3x3_halo_tiles(g), gp, w + (int64_t)N * k_pad, amax0, amax1);
+  hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true, BN == 64>), dim3((unsigned)(gp * n_tiles)),
+                     dim3(HTHREADS), 0, st, g, w, N, k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g),
+                     gp, w + (int64_t)N * k_pad, amax0, amax1);
 }
 
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st) {
-  // the register epilogue of the 64-column tiles keeps each tile in one output of a SPLIT
-  SELUNET_REQUIRE(ep.mode != SELUNET_EP_SPLIT || ep.split % 64 == 0, "conv3x3_x2: split %d is not a multiple of 64",
-                  ep.split);
   if (conv3x3_wino_bn128(N, ep)) launch_x2<128>(g, w, N, ep, amax0, amax1, st);
   else launch_x2<64>(g, w, N, ep, amax0, amax1, st);
   return check_launch("conv3x3_x2");

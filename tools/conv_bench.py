@@ -5,7 +5,7 @@
 
 Calls selunet_gemm_gather directly on random NHWC operands (forward: BN+ReLU transform of the
 producer applied on load, BN-stat epilogue; dgrad: untransformed dY, the SPLIT epilogue where the
-layer's input was a concatenation) and reports TFLOP/s per layer and the total.
+layer's input was a concatenation, the BN-backward sums of the producer otherwise) and reports TFLOP/s per layer and the total.
 """
 import argparse
 import ctypes
@@ -50,6 +50,15 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
         o0 = torch.empty(m, co // 2, device=dev, dtype=dt)
         o1 = torch.empty(m, co // 2, device=dev, dtype=dt)
         ep = K.Epilogue(o0.data_ptr(), o1.data_ptr(), None, None, K.EP_SPLIT, co // 2)
+    elif not transform:  # data gradient into a BatchNorm layer: the BN-backward sums (reads its y)
+        o0 = torch.empty(m, co, device=dev, dtype=dt)
+        o1 = None
+        yp = torch.randn(m, co, device=dev).to(dt)
+        cf = [torch.rand(co, device=dev) + 0.5 for _ in range(4)]
+        slab = torch.empty(rows, 3, co, device=dev)
+        keep += [yp, slab, *cf]
+        ep = K.Epilogue(o0.data_ptr(), None, None, None, K.EP_PLAIN, 0)
+        ep.bnb = K.BnBwdStats(K.ptr(yp), *(K.ptr(t) for t in cf), K.ptr(slab))
     else:
         o0 = torch.empty(m, co, device=dev, dtype=dt)
         o1 = None
