@@ -296,7 +296,35 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
   float* t1 = WIDE ? tw1 : reinterpret_cast<float*>(s1);
   float* t2 = WIDE ? tw2 : reinterpret_cast<float*>(s2);
   float* t3 = WIDE ? tw3 : reinterpret_cast<float*>(s3);
-  for (int row = r0; row < TR; row += RS) {
+  // rows of this thread: r0, r0 + RS, ... (TR % RS == 0). With BN-backward sums, each batch of YB
+  // rows loads its y before any of its stores (the stores may alias y as far as the compiler knows,
+  // so a load between them waits one memory latency per row): 2-4 % on the 128-column data
+  // gradients with 4 rows; the 64-column persistent conv spills with 4 and takes 2 (1 %)
+  constexpr int NR = TR / RS;
+  constexpr int YB = NR < (TC >= 128 ? 4 : 2) ? NR : (TC >= 128 ? 4 : 2);
+  static_assert(TR % RS == 0 && NR % YB == 0, "epilogue rows must split evenly over the threads");
+#pragma unroll 1
+  for (int rb = 0; rb < NR; rb += YB) {
+  T yb[YB][8];
+  if (do_bn) {
+#pragma unroll
+    for (int j = 0; j < YB; ++j) {
+      const T* p = dst(r0 + (rb + j) * RS, col);
+      if (p == nullptr) continue;
+      const T* yp = reinterpret_cast<const T*>(ts.bnb.y) + (p - reinterpret_cast<const T*>(ts.out0));
+      if constexpr (sizeof(T) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4*>(yp);
+        __builtin_memcpy(yb[j], &u, 16);
+      } else {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(yp), b = *reinterpret_cast<const f32x4*>(yp + 4);
+        __builtin_memcpy(yb[j], &a, 16);
+        __builtin_memcpy(yb[j] + 4, &b, 16);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < YB; ++j) {
+    const int row = r0 + (rb + j) * RS;
     T* p = dst(row, col);
     if (p == nullptr) continue;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(tile + row * (TC + 4) + col);
@@ -332,19 +360,9 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       for (int e = 0; e < 8; ++e) t1[e] += to_f(o[e]);
     }
     if (do_bn) {
-      const T* yp = reinterpret_cast<const T*>(ts.bnb.y) + (p - reinterpret_cast<const T*>(ts.out0));
-      T yv[8];
-      if constexpr (sizeof(T) == 2) {
-        const uint4 u = *reinterpret_cast<const uint4*>(yp);
-        __builtin_memcpy(yv, &u, 16);
-      } else {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(yp), b = *reinterpret_cast<const f32x4*>(yp + 4);
-        __builtin_memcpy(yv, &a, 16);
-        __builtin_memcpy(yv + 4, &b, 16);
-      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float y = to_f(yv[e]);
+        const float y = to_f(yb[j][e]);
         const float da = y * sc[e] + sh[e] > 0.0f ? to_f(o[e]) : 0.0f;
         const float xh = (y - mu[e]) * is[e];
         t1[e] += da;
@@ -352,6 +370,7 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
         t3[e] += xh;
       }
     }
+  }
   }
   if constexpr (WIDE) {
 #pragma unroll
