@@ -1184,7 +1184,7 @@ extern "C" const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mo
   EpiArg e{};
   e.mode = mode;
   e.split = split;
-  return conv3x3_wino_bn128(n_cols, e) ? "conv3x3_x2<f32,128>" : "conv3x3_x2<f32,64>";
+  return conv3x3_x2_bn128(n_cols, e) ? "conv3x3_x2<f32,128>" : "conv3x3_x2<f32,64>";
 }
 
 extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,

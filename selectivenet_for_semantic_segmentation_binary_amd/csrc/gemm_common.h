@@ -450,6 +450,7 @@ int64_t conv3x3_wgrad_wino_splits(const GatherArg& p, const GatherArg& q, int64_
 int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldw, hipStream_t st);
 bool conv3x3_wino_eligible(const GatherArg& g, int N);
 bool conv3x3_wino_bn128(int N, const EpiArg& ep);
+bool conv3x3_x2_bn128(int N, const EpiArg& ep);
 int conv3x3_wino_launch(const GatherArg& g, const float* u, int N, const EpiArg& ep, hipStream_t st);
 // fp32 forward / data gradient on split-fp16 operands (conv3x3.hip, selunet_conv3x3_x2)
 bool conv3x3_x2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
