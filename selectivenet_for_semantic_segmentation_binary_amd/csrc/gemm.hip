@@ -483,27 +483,30 @@ gemm_wgrad_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, in
 // ds_read_b64_tr_b16 operand reads) with each fp32 operand column scaled by its source's 2^e and
 // stored as two fp16 planes (high, low); three v_mfma_f32_32x32x16_f16 per 16-pixel step (hl, lh,
 // hh); each output (i, j) is unscaled by its two columns' 2^-e before the split partial is written.
-template <int BI, int BJ>
-__global__ void __launch_bounds__(256, 2)
+// NTH = 512: 256-column tiles on 8 waves (2 x 4), one workgroup per CU — the ConvTranspose2d weight
+// gradients re-read each operand once per tile of the other, so wider tiles halve that traffic.
+template <int BI, int BJ, int NTH = 256>
+__global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1)
 gemm_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int64_t mchunk, int tiles_j, int tiles, float* __restrict__ ws,
                      int64_t ws_stride, const float* __restrict__ amax_p0, const float* __restrict__ amax_p1,
                      const float* __restrict__ amax_q0, const float* __restrict__ amax_q1) {
   constexpr int KM = 32;                           // pixels per stage
   constexpr int PADE = 32;                         // 64 B row pad (bank spread for tr reads)
   constexpr int LDI = BI + PADE, LDJ = BJ + PADE;  // row strides in halves
-  constexpr int WI = BI / 2, WJ = BJ / 2;
+  constexpr int WGJ = NTH / 128;                   // waves along j (2 along i)
+  constexpr int WI = BI / 2, WJ = BJ / WGJ;
   constexpr int MT = WI / 32, NT = WJ / 32;
   constexpr int CPI = BI / 4, CPJ = BJ / 4;        // 16-B fp32 chunks per row
-  constexpr int RPI = 256 / CPI, RPJ = 256 / CPJ;
+  constexpr int RPI = NTH / CPI, RPJ = NTH / CPJ;
   constexpr int PI = KM / RPI, PJ = KM / RPJ;
-  static_assert(PI >= 1 && PJ >= 1, "stage rows must cover the threads");
+  static_assert(PI >= 1 && PJ >= 1 && MT >= 1 && NT >= 1, "stage rows must cover the threads");
 
   __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][KM][LDI];
   __shared__ __attribute__((aligned(16))) _Float16 Qs[2][2][KM][LDJ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
+  const int wi = wave / WGJ, wj = wave % WGJ;
   const int half = lane >> 5, l32 = lane & 31;
   const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
@@ -912,14 +915,15 @@ static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out
                               float* ws, hipStream_t st);
 
 // pixel splits of the generic weight gradient (rows per split a multiple of the 64-pixel stage)
-static int64_t wgrad_splits(int64_t M, int tiles, int64_t* mchunk_out) {
+static int64_t wgrad_splits(int64_t M, int tiles, int64_t* mchunk_out, int64_t wgs = 0) {
   // workgroup target over (tile, pixel split): 512 (two per CU) measured 6.43 vs 6.57 ms/step at
   // 16 images/GPU against 2048 (fewer split partials to reduce), equal at 128; 256 and 1024 in
-  // between (SELUNET_GEMM_WGRAD_WGS overrides)
-  static const int64_t target = [] {
+  // between (SELUNET_GEMM_WGRAD_WGS overrides); wgs: a kernel's own target (one workgroup per CU)
+  static const int64_t target_env = [] {
     const char* e = getenv("SELUNET_GEMM_WGRAD_WGS");
     return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)512;
   }();
+  const int64_t target = wgs > 0 ? wgs : target_env;
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(target, tiles)));
   const int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
   if (mchunk_out) *mchunk_out = mchunk;
@@ -1500,12 +1504,22 @@ extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_g
 
 // generic fp32 weight gradient on split-fp16 operands (gemm_wgrad_x2_kernel + the fixed-order split
 // reduction into the reference layout)
+// tile of the generic split-fp16 weight gradient: 256 columns (512 threads, one workgroup per CU)
+// where the operands allow, else 128 / 64 (256 threads, two per CU)
+struct Gx2Tile {
+  int bi, bj, nth;
+};
+static Gx2Tile gx2_tile(const WgradPlan& w) {
+  if (w.nj_pad % 256 == 0 && (w.ni % 256 == 0 || w.ni == 128)) return {w.ni % 256 == 0 ? 256 : 128, 256, 512};
+  return {w.ni % 128 == 0 ? 128 : 64, w.bj, 256};
+}
+
 static int plan_wgrad_gx2(const selunet_gather* p, const selunet_gather* q, WgradPlan& w) {
   if (int rc = plan_wgrad(p, q, SELUNET_F32, w)) return rc;
   SELUNET_REQUIRE(!w.gp.small && !w.gq.small && w.gp.K % 64 == 0 && w.gq.K % 64 == 0,
                   "gemm_wgrad_x2: vector gathers with K_p, K_q multiples of 64 (got %d, %d)", w.gp.K, w.gq.K);
-  const int bi = w.ni % 128 == 0 ? 128 : 64;
-  w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
+  const Gx2Tile t = gx2_tile(w);
+  w.splits = wgrad_splits(w.gp.M, (w.ni / t.bi) * (w.nj_pad / t.bj), nullptr, t.nth == 512 ? 256 : 0);
   return 0;
 }
 
@@ -1528,13 +1542,20 @@ extern "C" int selunet_gemm_wgrad_x2(const selunet_gather* p, const selunet_gath
   SELUNET_REQUIRE(amax_p0 && amax_q0 && (p->nsrc == 1 || amax_p1) && (q->nsrc == 1 || amax_q1),
                   "gemm_wgrad_x2: every operand source needs its range word");
   hipStream_t st = as_stream(stream);
-  const int bi = w.ni % 128 == 0 ? 128 : 64;
-  const int tiles_j = w.nj_pad / w.bj, tiles = (w.ni / bi) * tiles_j;
+  const Gx2Tile t = gx2_tile(w);
+  const int bi = t.bi;
+  const int tiles_j = w.nj_pad / t.bj, tiles = (w.ni / bi) * tiles_j;
   int64_t mchunk;
-  wgrad_splits(w.gp.M, tiles, &mchunk);
+  wgrad_splits(w.gp.M, tiles, &mchunk, t.nth == 512 ? 256 : 0);
   const unsigned blocks = (unsigned)(tiles * w.splits);
   const int64_t stride = (int64_t)w.ni * w.nj_pad;
-  if (bi == 128 && w.bj == 128)
+  if (t.nth == 512 && bi == 256)
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<256, 256, 512>), dim3(blocks), dim3(512), 0, st, w.gp, w.gq, w.nj_pad,
+                       mchunk, tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  else if (t.nth == 512)
+    hipLaunchKernelGGL((gemm_wgrad_x2_kernel<128, 256, 512>), dim3(blocks), dim3(512), 0, st, w.gp, w.gq, w.nj_pad,
+                       mchunk, tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
+  else if (bi == 128 && w.bj == 128)
     hipLaunchKernelGGL((gemm_wgrad_x2_kernel<128, 128>), dim3(blocks), dim3(256), 0, st, w.gp, w.gq, w.nj_pad, mchunk,
                        tiles_j, tiles, ws, stride, amax_p0, amax_p1, amax_q0, amax_q1);
   else if (w.bj == 128)

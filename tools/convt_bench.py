@@ -1,5 +1,5 @@
 """Time the ConvTranspose2d GEMMs (selunet_gemm_gather SCATTER2X forward, taps=4 dgrad) at the
-bench shapes (bs=128, bf16; --x2: the fp32 split-fp16 kernels) — profiling tool, like tools/conv_bench.py.
+bench shapes (bs=128, bf16; --x2: the fp32 split-fp16 kernels and the weight gradient) — profiling tool, like tools/conv_bench.py.
 
     python tools/convt_bench.py [--batch 128] [--iters 10] [--x2]
 """
@@ -82,6 +82,19 @@ def main():
         tot += ms
         print(f"dgrad {name} {co}->{ci} @{r}: {ms:.3f} ms  {2 * n * r * r * ci * 4 * co / ms / 1e9:7.1f} TF/s "
               f"{byt / ms / 1e6:7.1f} GB/s", flush=True)
+        if a.x2:  # weight gradient: P = the layer input (BN+ReLU of its producer), Q = dU gathered per 2x2 tap
+            gp = K.gather(n, r, r, 1, K.source(x, ci, sc, sh))
+            gq = K.gather(n, r, r, 4, K.source(du, co))
+            wsb = K.query("selunet_gemm_wgrad_x2_ws_bytes", gp, gq)
+            ws = torch.empty(max(wsb // 4, 1), device=dev)
+            gw = torch.empty(ci, co, 2, 2, device=dev)
+            fw = lambda: K.call("selunet_gemm_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.WG_CONVT, K.ptr(gw),  # noqa: E731
+                                K.ptr(amax), None, K.ptr(amax), None, K.stream_ptr())
+            ms = timed(fw, a.iters)
+            byt = (x.numel() + du.numel()) * 4
+            tot += ms
+            print(f"wgrad {name} {ci}x{co}x4 @{r}: {ms:.3f} ms  {2 * n * r * r * ci * 4 * co / ms / 1e9:7.1f} TF/s "
+                  f"{byt / ms / 1e6:7.1f} GB/s", flush=True)
     print(f"total {tot:.3f} ms")
 
 
