@@ -46,10 +46,14 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
     m = n * hw * hw
     rows = K.query("selunet_gemm_stats_rows", ctypes.byref(g), co, K.dtype_code(dt))
     stats = torch.empty(rows, 2, co, device=dev) if not split else None
-    if split:
+    if split:  # as in the step: the ConvTranspose2d bias sums of out0 and its range word
         o0 = torch.empty(m, co // 2, device=dev, dtype=dt)
         o1 = torch.empty(m, co // 2, device=dev, dtype=dt)
-        ep = K.Epilogue(o0.data_ptr(), o1.data_ptr(), None, None, K.EP_SPLIT, co // 2)
+        colsum = torch.empty(rows, co // 2, device=dev)
+        amo = torch.zeros(1, device=dev)
+        keep += [colsum, amo]
+        ep = K.Epilogue(o0.data_ptr(), o1.data_ptr(), None, None, K.EP_SPLIT, co // 2, K.ptr(colsum))
+        ep.amax = K.ptr(amo)
     elif not transform:  # data gradient into a BatchNorm layer: the BN-backward sums (reads its y)
         o0 = torch.empty(m, co, device=dev, dtype=dt)
         o1 = None
