@@ -169,6 +169,16 @@ convt_x2_kernel(GatherArg g, const float* __restrict__ W, int N, EpiArg ep, int 
   const int Cq = N / 4;  // C_out
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     float* out = reinterpret_cast<float*>(ep.out0);
+    // the columns' bias and unscale (weight row) x 2^-e, loaded before any store: `out` may alias
+    // them as far as the compiler knows, so loads between the stores would each wait a full memory
+    // latency (8 per tile)
+    float cbias[NT], ccf[NT];
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int n = n0 + b * 32 + l32;
+      cbias[b] = ep.bias ? ep.bias[n % Cq] : 0.0f;
+      ccf[b] = wcs[n] * inv;
+    }
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
       const int64_t r0 = sub_row0(t, a);
@@ -181,8 +191,8 @@ convt_x2_kernel(GatherArg g, const float* __restrict__ W, int N, EpiArg ep, int 
       for (int b = 0; b < NT; ++b) {
         const int n = n0 + b * 32 + l32;
         const int ab = n / Cq, o = n - ab * Cq;
-        const float bias = ep.bias ? ep.bias[o] : 0.0f;
-        const float cf = wcs[n] * inv;  // the column's unscale (weight row) x 2^-e
+        const float bias = cbias[b];
+        const float cf = ccf[b];
         const int64_t base = row_even + (int64_t)(ab >> 1) * (2 * g.w) + (ab & 1);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
