@@ -411,6 +411,14 @@ int selunet_first_conv_fwd(const float* x, int32_t n, int32_t cin, int32_t h, in
 int64_t selunet_first_conv_wgrad_rows(int32_t n, int32_t h, int32_t w);
 int selunet_first_conv_wgrad(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
                              float* slab, int32_t dtype, void* stream);
+/* The same weight gradient with encoder_layer_1_1's BatchNorm+ReLU backward fused into the staging:
+ * dz = dA of the layer, y its conv output, scale/shift/mean/invstd its BN, coef [3][64] from
+ * selunet_bn_bwd_stats_finalize; dy = (y*scale+shift > 0 ? k0*dz : 0) - b - a*y exactly as
+ * selunet_bn_bwd_apply forms it, never written (replaces selunet_bn_bwd_apply + selunet_first_conv_wgrad,
+ * whose dy has no other reader: the input needs no gradient, model.py:29 / train.py:207). */
+int selunet_first_conv_wgrad_bn(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dz,
+                                const void* y, const float* scale, const float* shift, const float* mean,
+                                const float* invstd, const float* coef, float* slab, int32_t dtype, void* stream);
 
 /* ---- MaxPool2d(2) on relu(bn(y)) (model.py:31,35,39) ---------------------------------- */
 int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,

@@ -137,6 +137,8 @@ SIGNATURES = {
                                                     P, P]),
     "selunet_first_conv_wgrad_rows": (c_int64, [c_int32, c_int32, c_int32]),
     "selunet_first_conv_wgrad": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, c_int32, P]),
+    "selunet_first_conv_wgrad_bn": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, P, P, P, c_int32,
+                                              P]),
     "selunet_heads_fwd": (c_int32, [P, c_int64, P, P, P, P, c_int32, P, P, P, c_int32, P]),
     "selunet_heads_bwd": (c_int32, [P, c_int64, P, P, P, c_int32, P, P, P, P, P, ctypes.POINTER(BnBwdStats),
                                     c_int32, P]),

@@ -181,10 +181,23 @@ first_conv_fwd_kernel(const float* __restrict__ x, int cin, int h, int w, const 
 }
 
 // ---------------------------------------------------------------------------------- wgrad
-template <typename T>
+// BNA: the layer's BatchNorm+ReLU backward applied while staging — the kernel reads dA (`dy`) and the
+// layer's conv output y and forms dy = (y sc + sh > 0 ? k0 dA : 0) - b - a y as selunet_bn_bwd_apply
+// does (its coefficients from coef / invstd / mean), so encoder_layer_1_1's dy, which nothing else
+// reads, is never written: one read pass of dA and y instead of apply (read both, write dy) + read dy.
+struct FirstBnApply {
+  const void* y;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  const float* coef;  // [3][64] k0, k1, k2 (selunet_bn_bwd_stats_finalize)
+};
+
+template <typename T, bool BNA = false>
 __global__ void __launch_bounds__(FTHREADS, 2)
 first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ dy, float* slab,
-                        int tiles_x, int tiles_y, int total_tiles, int tiles_per_block) {
+                        int tiles_x, int tiles_y, int total_tiles, int tiles_per_block, FirstBnApply bna) {
   // a tile runs as two stages of HP = 128 pixels (tile rows 0-7, 8-15): 54 KB of LDS, two workgroups
   // per CU (a whole-tile stage needed 104 KB: one workgroup, every phase exposed)
   constexpr int HP = FPIX / 2;
@@ -193,10 +206,11 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
   constexpr int CH = FCO / 2;                    // dY channels per thread: two threads per pixel
   constexpr int DV = CH / E;                     // 16-B vectors per thread and stage
   constexpr int XR = (3 * FH * FH + FTHREADS - 1) / FTHREADS;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[FCO * PB + FK * PB + 3 * FH * FH * 4];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[FCO * PB + FK * PB + 3 * FH * FH * 4 + (BNA ? 5 * FCO * 4 : 0)];
   unsigned char* Ds = smem;                        // [64 co][128 px]
   unsigned char* Cs = smem + FCO * PB;             // [32 k][128 px]
   float* Xs = reinterpret_cast<float*>(Cs + FK * PB);
+  float* Kc = Xs + 3 * FH * FH;                    // BNA: [5][64] sc, sh, k0, a, b
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
@@ -207,6 +221,7 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
 
   struct Loaded {
     uint4 d[DV];
+    uint4 yv[BNA ? DV : 1];
     float xh[XR];
   };
   // job j = (tile tb + j / 2, stage j % 2): this thread's dY channels of its pixel, and at stage 0
@@ -221,6 +236,11 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
     const T* src = dy + (((int64_t)img * h + y) * w + xx) * FCO + hc * CH;
 #pragma unroll
     for (int v = 0; v < DV; ++v) L.d[v] = *reinterpret_cast<const uint4*>(src + v * E);
+    if constexpr (BNA) {
+      const T* ysrc = reinterpret_cast<const T*>(bna.y) + (((int64_t)img * h + y) * w + xx) * FCO + hc * CH;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) L.yv[v] = *reinterpret_cast<const uint4*>(ysrc + v * E);
+    }
     if (st == 0) {
 #pragma unroll
       for (int r = 0; r < XR; ++r) {
@@ -256,6 +276,17 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
     for (int v = 0; v < DV; ++v) {
       T e[E];
       __builtin_memcpy(e, &L.d[v], 16);
+      if constexpr (BNA) {
+        T yq[E];
+        __builtin_memcpy(yq, &L.yv[v], 16);
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+          const int c = hc * CH + v * E + q;  // (one channel half per wave: the reads broadcast)
+          const float yy = to_f(yq[q]);
+          e[q] = from_f<T>((yy * Kc[c] + Kc[FCO + c] > 0.0f ? Kc[2 * FCO + c] * to_f(e[q]) : 0.0f) - Kc[4 * FCO + c] -
+                           Kc[3 * FCO + c] * yy);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < E; ++q) dcol[(hc * CH + v * E + q) * (PB / (int)sizeof(T))] = inside ? e[q] : from_f<T>(0.0f);
     }
@@ -279,6 +310,17 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
 
   f32x16 acc = f32x16{};
   const int jobs = 2 * (te - tb);
+  if constexpr (BNA) {
+    for (int c = tid; c < FCO; c += FTHREADS) {
+      const float k2i = bna.coef[2 * FCO + c] * bna.invstd[c];
+      Kc[c] = bna.scale[c];
+      Kc[FCO + c] = bna.shift[c];
+      Kc[2 * FCO + c] = bna.coef[c];
+      Kc[3 * FCO + c] = k2i;
+      Kc[4 * FCO + c] = bna.coef[FCO + c] - k2i * bna.mean[c];
+    }
+    __syncthreads();
+  }
   if (jobs > 0) {
     Loaded cur = load(0);
     for (int j = 0; j < jobs; ++j) {
@@ -359,21 +401,46 @@ extern "C" int64_t selunet_first_conv_wgrad_rows(int32_t n, int32_t h, int32_t w
   return cdiv(total, wgrad_tiles_per_block(total));
 }
 
-extern "C" int selunet_first_conv_wgrad(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
-                                        float* slab, int32_t dtype, void* stream) {
+static int first_wgrad_launch(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
+                              float* slab, int32_t dtype, const FirstBnApply* bna, void* stream) {
   SELUNET_REQUIRE(x && dy && slab && n > 0 && h > 0 && w > 0 && cin >= 1 && cin <= 3, "first_conv_wgrad: bad arguments");
   SELUNET_REQUIRE((int64_t)n * cdiv(h, FT) * cdiv(w, FT) < (int64_t(1) << 31), "first_conv_wgrad: grid too large");
   int tx, ty;
   const int total = tiles_of(n, h, w, tx, ty);
   const int per = wgrad_tiles_per_block(total);
   const unsigned blocks = (unsigned)cdiv(total, per);
-  if (dtype == SELUNET_F32)
-    hipLaunchKernelGGL(first_conv_wgrad_kernel<float>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h,
-                       w, reinterpret_cast<const float*>(dy), slab, tx, ty, total, per);
-  else if (dtype == SELUNET_BF16)
-    hipLaunchKernelGGL(first_conv_wgrad_kernel<__bf16>, dim3(blocks), dim3(FTHREADS), 0, as_stream(stream), x, cin, h,
-                       w, reinterpret_cast<const __bf16*>(dy), slab, tx, ty, total, per);
-  else
+  const FirstBnApply none{};
+  hipStream_t st = as_stream(stream);
+  if (dtype == SELUNET_F32) {
+    if (bna)
+      hipLaunchKernelGGL((first_conv_wgrad_kernel<float, true>), dim3(blocks), dim3(FTHREADS), 0, st, x, cin, h, w,
+                         reinterpret_cast<const float*>(dy), slab, tx, ty, total, per, *bna);
+    else
+      hipLaunchKernelGGL((first_conv_wgrad_kernel<float, false>), dim3(blocks), dim3(FTHREADS), 0, st, x, cin, h, w,
+                         reinterpret_cast<const float*>(dy), slab, tx, ty, total, per, none);
+  } else if (dtype == SELUNET_BF16) {
+    if (bna)
+      hipLaunchKernelGGL((first_conv_wgrad_kernel<__bf16, true>), dim3(blocks), dim3(FTHREADS), 0, st, x, cin, h, w,
+                         reinterpret_cast<const __bf16*>(dy), slab, tx, ty, total, per, *bna);
+    else
+      hipLaunchKernelGGL((first_conv_wgrad_kernel<__bf16, false>), dim3(blocks), dim3(FTHREADS), 0, st, x, cin, h, w,
+                         reinterpret_cast<const __bf16*>(dy), slab, tx, ty, total, per, none);
+  } else {
     return fail(SELUNET_EINVAL, "first_conv_wgrad: bad dtype %d", dtype);
+  }
   return check_launch("first_conv_wgrad");
+}
+
+extern "C" int selunet_first_conv_wgrad(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dy,
+                                        float* slab, int32_t dtype, void* stream) {
+  return first_wgrad_launch(x, n, cin, h, w, dy, slab, dtype, nullptr, stream);
+}
+
+extern "C" int selunet_first_conv_wgrad_bn(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, const void* dz,
+                                           const void* y, const float* scale, const float* shift, const float* mean,
+                                           const float* invstd, const float* coef, float* slab, int32_t dtype,
+                                           void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && mean && invstd && coef, "first_conv_wgrad_bn: BatchNorm operands missing");
+  const FirstBnApply bna{y, scale, shift, mean, invstd, coef};
+  return first_wgrad_launch(x, n, cin, h, w, dz, slab, dtype, &bna, stream);
 }

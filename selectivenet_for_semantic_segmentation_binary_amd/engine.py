@@ -580,6 +580,21 @@ class Engine:
         K.call("selunet_bn_bwd_stats_finalize", K.ptr(dg.slab), dg.rows, K.ptr(ws), None, M, co, K.ptr(gamma),
                K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]),
                K.ptr(coef), self.stream)
+        if first_x is not None:
+            # encoder_layer_1_1: its dy feeds only the weight gradient (the input needs none), which
+            # forms it from dA and y while staging (selunet_first_conv_wgrad_bn): dy is never written
+            cin = first_x.shape[1]
+            rows = K.query("selunet_first_conv_wgrad_rows", st.n, st.h, st.w)
+            slab = K.keep(torch.empty(rows, co, FIRST_KPAD, dtype=torch.float32, device=dev))
+            K.call("selunet_first_conv_wgrad_bn", K.ptr(first_x), st.n, cin, st.h, st.w, K.ptr(dg.t), K.ptr(st.y),
+                   K.ptr(st.scale), K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(slab),
+                   self.code, self.stream)
+            packed = K.keep(torch.empty(co, FIRST_KPAD, dtype=torch.float32, device=dev))
+            self._reduce(slab, rows, co * FIRST_KPAD, out32=packed)
+            K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, cin, FIRST_KPAD, K.ptr(G[f"{name}.0.weight"]),
+                   self.stream)
+            K.marker(("grads", name))
+            return None
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         wp = ctx.wpack[name]
         dyw = self._word(ctx, "dy:" + name) if wp.mode == "x2" else None
@@ -590,18 +605,6 @@ class Engine:
             K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                    K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
         # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
-        if first_x is not None:
-            cin = first_x.shape[1]
-            rows = K.query("selunet_first_conv_wgrad_rows", st.n, st.h, st.w)
-            slab = K.keep(torch.empty(rows, co, FIRST_KPAD, dtype=torch.float32, device=dev))
-            K.call("selunet_first_conv_wgrad", K.ptr(first_x), st.n, cin, st.h, st.w, K.ptr(dy), K.ptr(slab),
-                   self.code, self.stream)
-            packed = K.keep(torch.empty(co, FIRST_KPAD, dtype=torch.float32, device=dev))
-            self._reduce(slab, rows, co * FIRST_KPAD, out32=packed)
-            K.call("selunet_unpack_conv3x3_grad", K.ptr(packed), co, cin, FIRST_KPAD, K.ptr(G[f"{name}.0.weight"]),
-                   self.stream)
-            K.marker(("grads", name))
-            return None
         ci = sum(s.channels for s in input_srcs)
         ld = K.query("selunet_wgrad_ld", q_taps * ci)
         gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))

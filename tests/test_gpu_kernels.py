@@ -653,6 +653,32 @@ def test_first_conv_fwd_and_wgrad(dt, cin, n, h, w):
     assert rel(gw.cpu(), ref_w) < (TOL if dt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("dt,cin,n,h,w", [(torch.float32, 3, 2, 32, 32), (torch.float32, 2, 1, 20, 40),
+                                          (torch.bfloat16, 3, 2, 32, 48)])
+def test_first_conv_wgrad_bn_fused(dt, cin, n, h, w):
+    """selunet_first_conv_wgrad_bn (encoder_layer_1_1's BN+ReLU backward formed while staging) against
+    selunet_bn_bwd_apply + selunet_first_conv_wgrad on the same dA, y and coefficients: the same dy per
+    element, so the same partial sums (fp32: to rounding of the MFMA order; bf16: dy rounded alike)."""
+    M, co = n * h * w, 64
+    x = gen(n, cin, h, w, seed=70).to(DEV).contiguous()
+    dz = gen(M, co, seed=71).to(dt).to(DEV)
+    y = gen(M, co, seed=72).to(dt).to(DEV)
+    sc, sh = (gen(co, seed=73).abs() + 0.5).to(DEV), (gen(co, seed=74) * 0.3).to(DEV)
+    mean, invstd = (gen(co, seed=75) * 0.1).to(DEV), (gen(co, seed=76).abs() + 0.5).to(DEV)
+    coef = (gen(3, co, seed=77) * 0.2).to(DEV).contiguous()
+    dy = torch.empty(M, co, dtype=dt, device=DEV)
+    K.call("selunet_bn_bwd_apply", K.ptr(dz), K.ptr(y), M, co, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+           K.ptr(coef), K.ptr(dy), K.dtype_code(dt), K.stream_ptr())
+    rows = K.query("selunet_first_conv_wgrad_rows", n, h, w)
+    ref, got = torch.empty(rows, 64, 32, device=DEV), torch.empty(rows, 64, 32, device=DEV)
+    K.call("selunet_first_conv_wgrad", K.ptr(x), n, cin, h, w, K.ptr(dy), K.ptr(ref), K.dtype_code(dt), K.stream_ptr())
+    K.call("selunet_first_conv_wgrad_bn", K.ptr(x), n, cin, h, w, K.ptr(dz), K.ptr(y), K.ptr(sc), K.ptr(sh),
+           K.ptr(mean), K.ptr(invstd), K.ptr(coef), K.ptr(got), K.dtype_code(dt), K.stream_ptr())
+    torch.cuda.synchronize()
+    r, g = ref.double().sum(0).cpu(), got.double().sum(0).cpu()
+    assert rel(g, r) < (1e-6 if dt == torch.float32 else 1e-5)
+
+
 @pytest.mark.parametrize("cin0,cin1,cout,n,h,w", [
     (128, 0, 128, 2, 20, 72),    # partial tiles in both directions
     (64, 0, 64, 2, 40, 36),      # one channel chunk: weights-resident persistent kernel
