@@ -459,6 +459,11 @@ int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e
                       const float* amax1, hipStream_t st);
 // ConvTranspose2d forward on split-fp16 operands with resident weights (convt.hip)
 bool convt_x2_eligible(const GatherArg& g, int N, const EpiArg& e);
+int convt_dgrad_x2_ntb(const GatherArg& g, int N);
+int64_t convt_dgrad_x2_rows(const GatherArg& g, int N);
+bool convt_dgrad_x2_eligible(const GatherArg& g, int N, const EpiArg& e);
+int convt_dgrad_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
+                          hipStream_t st);
 int convt_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                     hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);

@@ -9,7 +9,9 @@ over real Adam steps runs agree to fp32 rounding, not bit for bit: step-0 head o
 relative (nothing has been updated yet); later steps' outputs 1e-2 relative to the tensor max and
 parameters within 5e-3 absolute (Adam normalises the update, so an element whose gradient is
 rounding noise moves by up to +-lr per step either way — the same bound the reference-parity
-tests use for later steps).
+tests use for later steps). Losses: steps 0-1 within 1e-6 relative; step 2, after two such
+updates, 1e-4 (measured: recorded and replayed runs are each bit-reproducible, and differ at step 2
+by 4e-7 to 1e-5 relative depending on which elements' noise-level gradients flip sign).
 """
 import gc
 
@@ -51,7 +53,8 @@ def test_replayed_steps_match_recorded_steps():
     eng = net._engine()
     assert sum(len(v) for v in eng._plans.values()) >= 1 and all(e.plan is not None for v in eng._plans.values()
                                                                    for e in v)
-    assert np.allclose(l_on, l_off, rtol=1e-5, atol=0), (l_on, l_off)
+    assert np.allclose(l_on[:2], l_off[:2], rtol=1e-6, atol=0), (l_on, l_off)
+    assert np.allclose(l_on[2:], l_off[2:], rtol=1e-4, atol=0), (l_on, l_off)
     assert np.abs(o_on[0] - o_off[0]).max() <= 1e-4 * max(1.0, np.abs(o_off[0]).max())
     for a, b in zip(o_on[1:], o_off[1:]):
         assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())

@@ -332,6 +332,50 @@ def test_x2_convT_fwd_dgrad(cin, cout, gwgs, gather_wgs):
     check_bnb_sums(slab, da, yprev, sc, sh, mean, invstd)
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w", [(128, 64, 2, 9, 64), (256, 128, 2, 9, 64), (256, 128, 1, 5, 32),
+                                             (128, 64, 4, 72, 512)])
+def test_x2_convT_dgrad_resident(cin, cout, n, h, w):
+    """ConvTranspose2d data gradient on the resident-weight kernel (convt_dgrad_x2_kernel: K = 4*cout of
+    256 / 512, w % 32 == 0; partial last tiles, and several tiles per workgroup at 4x72x512) against torch
+    in fp64, with the BN-backward sums checked against the sums of its own output."""
+    x = gen(n, cin, h, w, seed=23)
+    a = x.double().requires_grad_()
+    wt = gen(cin, cout, 2, 2, seed=24, scale=0.05).double()
+    y = F.conv_transpose2d(a, wt, None, stride=2)
+    dy = gen(*y.shape, seed=25) * 1e-3
+    (ga,) = torch.autograd.grad(y, (a,), dy.double())
+    _, dg = pack_convT_x2(wt.float())
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    dud = d(nhwc(dy))
+    amd = word(dy.abs().max())
+    M = n * h * w
+    da = torch.empty(M, cin, device=DEV)
+    yprev = gen(M, cin, seed=47).to(DEV)
+    sc, sh = (gen(cin, seed=48).abs() + 0.5).to(DEV), (gen(cin, seed=49) * 0.3).to(DEV)
+    mean, invstd = (gen(cin, seed=50) * 0.1).to(DEV), (gen(cin, seed=51).abs() + 0.5).to(DEV)
+    g4 = K.gather(n, h, w, 4, K.source(dud, cout))
+    rows = K.query("selunet_gemm_gather_x2_stats_rows", g4, cin)
+    ntb = 128 if cout == 64 else 64
+    tile = 8 * (8 // (ntb // 32)) * 32
+    assert rows == min(-(-M // tile), 256 // (cin // ntb))  # the resident-weight kernel's workgroup rows
+    slab = torch.full((rows, 3, cin), float("nan"), device=DEV)
+    amo = torch.zeros(1, device=DEV)
+    ep = K.Epilogue(K.ptr(da), None, None, None, K.EP_PLAIN, 0)
+    ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+    ep.amax = K.ptr(amo)
+    K.call("selunet_gemm_gather_x2", g4, K.ptr(dg), cin, 4 * cout, ep, K.ptr(amd), None, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel(nchw(da.cpu(), n, h, w), ga) < TOL
+    assert amo.item() == da.abs().max().item()
+    y64, g64 = yprev.double(), da.double() * (yprev.double() * sc.double() + sh.double() > 0).double()
+    xh = (y64 - mean.double()) * invstd.double()
+    terms = [g64, g64 * xh, xh]
+    got = slab.double().sum(0)
+    for k in range(3):
+        err = (got[k] - terms[k].sum(0)).abs() / (terms[k].abs().sum(0) + 1e-30)
+        assert float(err.max()) < 1e-6, (k, float(err.max()))
+
+
 @pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64), (256, 128)])
 def test_x2_convT_wgrad(cin, cout):
     """ConvTranspose2d weight gradient through selunet_gemm_wgrad_x2 (split partials reduced into the
