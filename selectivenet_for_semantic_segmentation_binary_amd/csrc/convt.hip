@@ -228,7 +228,7 @@ convt_x2_kernel(GatherArg g, const float* __restrict__ W, int N, EpiArg ep, int 
     }
   }
 
-  if (ep.amax) atomic_amax(ep.amax, am);
+  if (ep.amax) block_amax(ep.amax, am, reinterpret_cast<float*>(smem));
 }
 
 // ConvTranspose2d data gradient (the backward of model.py:44-45, 51-52, 57-58): dX[(y, x)][ci] = sum over
@@ -443,7 +443,7 @@ convt_dgrad_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_blo
     }
   }
 
-  if (amax_out) atomic_amax(amax_out, am);
+  if (amax_out) block_amax(amax_out, am, reinterpret_cast<float*>(smem));
   if (do_bn) {
     // per-lane sums -> one slab row per workgroup (row prow, this block's columns), fixed order
     double* red = reinterpret_cast<double*>(smem);

@@ -392,9 +392,6 @@ constexpr int stats_flush_bytes() { return (NTHREADS / (TC / 8)) * TC * 3 * (int
 template <int TC, int NTHREADS, typename Acc>
 __device__ __forceinline__ void tile_stats_flush(float* red_f, int tid, const TileStats& ts, const Acc (&s1)[8],
                                                  const Acc (&s2)[8], const Acc (&s3)[8], float am) {
-  // the running max |stored value| of this thread's tiles: one atomic per wave per workgroup (an atomic
-  // per tile put 0.5M same-address atomics into a full-resolution launch)
-  if (ts.amax) atomic_amax(ts.amax, am);
   constexpr int CC = TC / 8;
   constexpr int RS = NTHREADS / CC;
   Acc* red = reinterpret_cast<Acc*>(red_f);
@@ -421,6 +418,9 @@ __device__ __forceinline__ void tile_stats_flush(float* red_f, int tid, const Ti
       else if (ts.gcol0 + c < ts.colsum_cols) ts.colsum[c] = a;
     }
   }
+  // the running max |stored value| of this thread's tiles: one atomic per workgroup (an atomic per tile
+  // put 0.5M same-address atomics into a full-resolution launch; one per wave, a 25-50 us tail)
+  if (ts.amax) block_amax(ts.amax, am, red_f);
 }
 
 template <typename T, int TR, int TC, int NTHREADS, typename Dst, typename BiasCol>

@@ -617,7 +617,8 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
     one(Vec4<T>::load(y + off), Vec4<T>::load(y + off + 4), Vec4<T>::load(dz + off), Vec4<T>::load(dz + off + 4),
         off);
   }
-  if (amax) atomic_amax(amax, am);
+  __shared__ float wred[TPB / 64];
+  if (amax) block_amax(amax, am, wred);
 }
 
 // selunet_act_bound: max_c |gamma_c| * sqrt(count) + max_c |beta_c| (one block)

@@ -1,6 +1,6 @@
-"""Time selunet_bn_bwd_apply(_amax) at the bs=128 fp32 shapes (profiling tool).
+"""Time selunet_bn_bwd_apply(_amax) at the fp32 shapes of a batch (profiling tool).
 
-    python tools/apply_bench.py [--iters 20]
+    python tools/apply_bench.py [--iters 20] [--batch 128]
 """
 import argparse
 import os
@@ -11,15 +11,17 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from selectivenet_for_semantic_segmentation_binary_amd import _lib as K  # noqa: E402
 
-SHAPES = [(128 * 256 * 256, 64), (128 * 128 * 128, 128), (128 * 64 * 64, 256), (128 * 32 * 32, 512)]
+SHAPES = [(256 * 256, 64), (128 * 128, 128), (64 * 64, 256), (32 * 32, 512)]  # pixels per image, C
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128)
     a = ap.parse_args()
     tot = 0.0
-    for m, c in SHAPES:
+    for px, c in SHAPES:
+        m = a.batch * px
         dz, y = torch.randn(m, c, device="cuda"), torch.randn(m, c, device="cuda")
         dy = torch.empty_like(dz)
         co = [torch.rand(c, device="cuda") + 0.5 for _ in range(4)] + [torch.randn(3 * c, device="cuda")]
