@@ -799,6 +799,17 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
 // =========================================================================== 1x1 heads (C = 64)
 // 16 lanes per pixel, 4 channels per lane; 4 pixels per wave instruction.
 constexpr int HU = 4;
+
+// Sum over each 16-lane row of the wave, in every lane of the row, by DPP moves (VALU): quad xor 1,
+// quad xor 2, half-row mirror, row mirror. A __shfl_xor butterfly compiles to ds_bpermute through the
+// LDS crossbar, each waited on in turn (12 per pixel group in heads_fwd).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
 template <typename T>
 __global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
                                  const float* __restrict__ shift, const float* __restrict__ w,
@@ -816,10 +827,7 @@ __global__ void heads_fwd_kernel(const T* __restrict__ y, int64_t m, const float
     float acc[3];
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
-      float a = z[0] * wv[h][0] + z[1] * wv[h][1] + z[2] * wv[h][2] + z[3] * wv[h][3];
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 16);
-      acc[h] = a;
+      acc[h] = row16_sum(z[0] * wv[h][0] + z[1] * wv[h][1] + z[2] * wv[h][2] + z[3] * wv[h][3]);
     }
     if (sub == 0) {
       o0[p] = acc[0] + b[0];
@@ -1066,9 +1074,7 @@ __global__ void heads_n_fwd_kernel(const T* __restrict__ y, int64_t m, const flo
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (k < hp.n) {
-        float a = z[0] * wv[k][0] + z[1] * wv[k][1] + z[2] * wv[k][2] + z[3] * wv[k][3];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 16);
+        const float a = row16_sum(z[0] * wv[k][0] + z[1] * wv[k][1] + z[2] * wv[k][2] + z[3] * wv[k][3]);
         if (sub == 0) hp.plane[k][img * hp.img_stride[k] + q] = a + b[k];
       }
     }
