@@ -195,15 +195,17 @@ struct FirstBnApply {
 };
 
 template <typename T, bool BNA = false>
-__global__ void __launch_bounds__(FTHREADS, 2)
+__global__ void __launch_bounds__(FTHREADS, 3)
 first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, const T* __restrict__ dy, float* slab,
                         int tiles_x, int tiles_y, int total_tiles, int tiles_per_block, FirstBnApply bna) {
-  // a tile runs as two stages of HP = 128 pixels (tile rows 0-7, 8-15): 54 KB of LDS, two workgroups
-  // per CU (a whole-tile stage needed 104 KB: one workgroup, every phase exposed)
-  constexpr int HP = FPIX / 2;
-  constexpr int PB = HP * (int)sizeof(T) + 16;  // transposed row bytes (128 pixels + pad)
+  // a tile runs as four stages of HP = 64 pixels (four tile rows each): 31 KB of LDS and 132 VGPRs
+  // (fp32, BN-backward fused), three workgroups per CU. Two 128-pixel stages (54 KB, 188 VGPRs: the
+  // next stage's dA and y held across the transform) ran two per CU; a whole-tile stage (104 KB) one
+  constexpr int NS = 4;                          // stages per tile
+  constexpr int HP = FPIX / NS;
+  constexpr int PB = HP * (int)sizeof(T) + 16;  // transposed row bytes (64 pixels + pad)
   constexpr int E = 16 / (int)sizeof(T);
-  constexpr int CH = FCO / 2;                    // dY channels per thread: two threads per pixel
+  constexpr int CH = FCO / NS;                   // dY channels per thread: four threads per pixel
   constexpr int DV = CH / E;                     // 16-B vectors per thread and stage
   constexpr int XR = (3 * FH * FH + FTHREADS - 1) / FTHREADS;
   __shared__ __attribute__((aligned(16))) unsigned char smem[FCO * PB + FK * PB + 3 * FH * FH * 4 + (BNA ? 5 * FCO * 4 : 0)];
@@ -214,8 +216,8 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
-  const int wa = wave & 1, wp = wave >> 1;  // co subtile, 64-pixel half of the stage
-  const int sp = tid % HP, hc = tid / HP;   // staging: stage pixel, channel (dY) / k (columns) half
+  const int wa = wave & 1, wp = wave >> 1;  // co subtile, 32-pixel half of the stage
+  const int sp = tid % HP, hc = tid / HP;   // staging: stage pixel, channel (dY) / k (columns) quarter
   const int tb = blockIdx.x * tiles_per_block;
   const int te = min(total_tiles, tb + tiles_per_block);
 
@@ -224,11 +226,11 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
     uint4 yv[BNA ? DV : 1];
     float xh[XR];
   };
-  // job j = (tile tb + j / 2, stage j % 2): this thread's dY channels of its pixel, and at stage 0
+  // job j = (tile tb + j / NS, stage j % NS): this thread's dY channels of its pixel, and at stage 0
   // the tile's input halo
   auto load = [&](int j) __attribute__((always_inline)) {
     Loaded L;
-    const int t = tb + (j >> 1), st = j & 1;
+    const int t = tb + j / NS, st = j % NS;
     int img, y0, x0;
     tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
     const int pix = st * HP + sp;
@@ -253,7 +255,7 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
     return L;
   };
   auto stage = [&](const Loaded& L, int j) __attribute__((always_inline)) {
-    const int t = tb + (j >> 1), st = j & 1;
+    const int t = tb + j / NS, st = j % NS;
     int img, y0, x0;
     tile_coords((unsigned)t, tiles_x, tiles_y, img, y0, x0);
     if (st == 0) {
@@ -291,14 +293,14 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
       for (int q = 0; q < E; ++q) dcol[(hc * CH + v * E + q) * (PB / (int)sizeof(T))] = inside ? e[q] : from_f<T>(0.0f);
     }
   };
-  // im2col columns k = 16 hc .. 16 hc + 15 of stage pixel sp
+  // im2col columns k = 8 hc .. 8 hc + 7 of stage pixel sp
   auto build_cols = [&](int st) __attribute__((always_inline)) {
     const int pix = st * HP + sp;
     const int py = pix / FT, px = pix % FT;
     T* ccol = reinterpret_cast<T*>(Cs) + sp;
 #pragma unroll
-    for (int kk = 0; kk < FK / 2; ++kk) {
-      const int k = hc * (FK / 2) + kk;
+    for (int kk = 0; kk < FK / NS; ++kk) {
+      const int k = hc * (FK / NS) + kk;
       float v = 0.0f;
       if (k < 9 * cin) {
         const int tap = k / cin, c = k - tap * cin;
@@ -309,7 +311,7 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
   };
 
   f32x16 acc = f32x16{};
-  const int jobs = 2 * (te - tb);
+  const int jobs = NS * (te - tb);
   if constexpr (BNA) {
     for (int c = tid; c < FCO; c += FTHREADS) {
       const float k2i = bna.coef[2 * FCO + c] * bna.invstd[c];
@@ -326,13 +328,13 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
     for (int j = 0; j < jobs; ++j) {
       stage(cur, j);
       __syncthreads();  // Xs, Ds written
-      build_cols(j & 1);
+      build_cols(j % NS);
       if (j + 1 < jobs) cur = load(j + 1);
       __syncthreads();  // Cs written
-      // out[co][k] += sum over this wave's 64 pixels of the stage
+      // out[co][k] += sum over this wave's 32 pixels of the stage
 #pragma unroll
-      for (int q = 0; q < 64 * (int)sizeof(T) / 32; ++q) {
-        const int boff = wp * 64 * (int)sizeof(T) + q * 32 + half * 16;
+      for (int q = 0; q < 32 * (int)sizeof(T) / 32; ++q) {
+        const int boff = wp * 32 * (int)sizeof(T) + q * 32 + half * 16;
         const uint4 af = *reinterpret_cast<const uint4*>(Ds + (wa * 32 + l32) * PB + boff);
         const uint4 bfr = *reinterpret_cast<const uint4*>(Cs + l32 * PB + boff);
         Mma<T>::run(acc, af, bfr);
