@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--no-full-loop", action="store_true")
     ap.add_argument("--no-input-loop", action="store_true", help="skip the timed loop fed by the patch loader")
     ap.add_argument("--layer-report", action="store_true", help="print per-entry-point timing to stderr")
+    ap.add_argument("--no-size512", action="store_true",
+                    help="skip the BASELINE configs[4] measurement (512x512, global bs=64, `size512` key)")
     return ap.parse_args()
 
 
@@ -473,6 +475,32 @@ def roofline(args, dtype, timer, ksteps, kel, local_batch):
     }
 
 
+def run_size512(args, world, rank, dev):
+    """BASELINE configs[4]: SelectiveUNet_B on 512x512 patches, global bs=64 split over the ranks as
+    the headline splits its 128 (DataParallel chunks), the same fp32 configuration and the same
+    barrier-bracketed max-over-ranks timing; the step alone (no per-kernel or loop passes)."""
+    import copy
+    a = copy.copy(args)
+    a.size, a.batch = 512, 64
+    a.no_kernel_timing = a.no_full_loop = a.no_input_loop = True
+    x, lab = make_batch(a.batch, a.size, seed=0)
+    lo, hi = parallel.chunk_bounds(a.batch, rank, world)
+    parallel.set_global_batch(a.batch)
+    xt = torch.tensor(x[lo:hi], device=dev)
+    lt = torch.tensor(lab[lo:hi], device=dev)
+    del x, lab
+    try:
+        r = run_config(a, args.dtype, world, rank, dev, xt, lt, hi - lo)
+    finally:
+        parallel.set_global_batch(args.batch)
+    r.pop("full_loop", None)
+    r["config"] = {"workload": f"SelectiveUNet_B train step, global bs=64, 512x512, Adam lr=1e-3, s_lamb={a.lamb:g}",
+                   "global_batch": 64, "per_gpu_batch": hi - lo, "image": 512, "parallelism": f"dp{world}"}
+    r["unit"] = "images/s"
+    r["step_tflops"] = round(TRAIN_GFLOP_PER_IMG_256 * 4 * r["value"] / 1e3, 2)
+    return r
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -508,6 +536,19 @@ def main():
             os.environ.pop("SELUNET_X2", None)
     if args.dtype == "fp32" and not args.no_bf16:
         extra = run_config(args, "bf16", world, rank, dev, xt, lt, hi - lo)
+    size512 = None
+    if not args.no_size512 and (args.size, args.batch) == (256, 128):
+        size512 = run_size512(args, world, rank, dev)
+    group = None
+    if world > 1:
+        # the group every rank ran in, as torch.distributed reports it on that rank
+        ws = torch.tensor([dist.get_world_size()], dtype=torch.int64, device=dev)
+        lo_ws, hi_ws = ws.clone(), ws.clone()
+        dist.all_reduce(lo_ws, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi_ws, op=dist.ReduceOp.MAX)
+        group = {"backend": str(dist.get_backend()), "world_size": int(ws.item()),
+                 "world_size_min_over_ranks": int(lo_ws.item()), "world_size_max_over_ranks": int(hi_ws.item()),
+                 "rccl": str(dist.get_backend()) == "nccl" and torch.version.hip is not None}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -542,7 +583,10 @@ def main():
             "final_loss": head["final_loss"], "peak_hbm_gb": head["peak_hbm_gb"],
             "full_loop": head.get("full_loop"), "input_loop": head.get("input_loop"),
             "roofline": head.get("roofline"), "cpu_baseline": cpu,
+            "process_group": group,
         }
+        if size512 is not None:
+            line["size512"] = size512
         if exact is not None:
             we = TRAIN_GFLOP_PER_IMG_256 * (args.size / 256) ** 2 * exact["value"] / 1e3
             # (direct-convolution FLOPs: the 1-D Winograd kernels execute 2/3 of them, so no fraction

@@ -38,6 +38,29 @@ enum {
   SELUNET_ELAUNCH = 2, /* HIP launch error */
 };
 
+/* Kernel-selection and tuning options (selunet_set_option). The library reads no environment
+ * variables; every value < 0 selects the built-in default. Selection options take 0/1. */
+enum {
+  SELUNET_OPT_HALO = 0,           /* 3x3 convolutions on the LDS halo kernels (1) or the gather GEMM (0) */
+  SELUNET_OPT_HALO_PERSIST,       /* persistent multi-chunk halo kernel (1) */
+  SELUNET_OPT_WINO,               /* exact-fp32 3x3 fwd/dgrad as 1-D Winograd F(2,3) (1) or direct (0) */
+  SELUNET_OPT_WINO_WGRAD,         /* exact-fp32 3x3 weight gradient as the Winograd transpose (1) */
+  SELUNET_OPT_WINO_WGRAD_TW,      /* its tile width: 16 (default) or 8 pixels */
+  SELUNET_OPT_WINO_WGRAD_WAVES,   /* its waves per workgroup: 12 (default) or 8 */
+  SELUNET_OPT_WGRAD_WGS,          /* workgroup target of the halo / Winograd weight gradients (256) */
+  SELUNET_OPT_X2_WGRAD_WGS,       /* workgroup target of the split-fp16 3x3 weight gradient (256) */
+  SELUNET_OPT_GEMM_WGRAD_WGS,     /* workgroup target of the generic weight gradient (512) */
+  SELUNET_OPT_GATHER_WGS,         /* resident gather-GEMM workgroups (512; 0 = one tile each) */
+  SELUNET_OPT_RF_SINGLE,          /* slab rows reduced in one launch by the fused reductions (1024) */
+  SELUNET_OPT_APPLY_U8,           /* BN-backward apply: 8 channel groups per thread (0) */
+  SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
+  SELUNET_OPT_COUNT
+};
+/* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
+ * unknown key. Changes apply to later calls (the stats-slab row counts of selunet_gemm_stats_rows
+ * follow SELUNET_OPT_HALO_PERSIST / GATHER_WGS). Not thread-safe; set before enqueuing work. */
+int64_t selunet_set_option(int32_t key, int64_t value);
+
 /* Rows of the GEMM output tile (pixels per workgroup); stats slabs have ceil(M/128) rows. */
 #define SELUNET_GEMM_BM 128
 
@@ -112,6 +135,8 @@ typedef struct selunet_epilogue {
 
 const char* selunet_last_error(void);
 int32_t selunet_version(void);
+/* Fingerprint (SHA-256 prefix) of the kernel sources, headers and flags this library was built from. */
+const char* selunet_build_id(void);
 
 /* ---- weight repacking (fp32 master weights -> GEMM operands, dtype) ---------------- */
 /* conv3x3 weight [co][ci][3][3] -> fwd [co][k_pad] (k = tap*ci + c, zero pad to k_pad) and,

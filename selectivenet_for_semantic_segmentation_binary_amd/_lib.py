@@ -72,6 +72,7 @@ P = c_void_p
 SIGNATURES = {
     "selunet_last_error": (ctypes.c_char_p, []),
     "selunet_version": (c_int32, []),
+    "selunet_build_id": (ctypes.c_char_p, []),
     "selunet_pack_conv3x3": (c_int32, [P, c_int32, c_int32, c_int32, P, P, c_int32, P]),
     "selunet_pack_convT": (c_int32, [P, c_int32, c_int32, P, P, c_int32, P]),
     "selunet_unpack_conv3x3_grad": (c_int32, [P, c_int32, c_int32, c_int32, P, P]),
@@ -172,6 +173,7 @@ SIGNATURES = {
     "selunet_prep_batch": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
     "selunet_prep_batch_mode": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
     "selunet_seg_metrics": (c_int32, [P, P, P, c_int64, c_float, c_float, P, P]),
+    "selunet_set_option": (c_int64, [c_int32, c_int64]),
 }
 
 _lib = None
@@ -201,12 +203,39 @@ def load(auto_build: bool = False):
                     "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`). "
                     "There is no CPU fallback.")
         L = ctypes.CDLL(path)
+        L.selunet_build_id.restype = ctypes.c_char_p
+        built_from = L.selunet_build_id().decode()
+        if "SELUNET_LIB" not in os.environ and built_from != _build.source_fingerprint():
+            raise RuntimeError(
+                f"{path} was built from other sources (build id {built_from}, tree "
+                f"{_build.source_fingerprint()}): rebuild with "
+                "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        for env, key in ENV_OPTIONS.items():  # the host's choices; the library reads no environment
+            v = os.environ.get(env)
+            if v is not None and v.strip().lstrip("-").isdigit():
+                L.selunet_set_option(key, int(v))
+        if os.environ.get("SELUNET_NO_HALO") == "1":
+            L.selunet_set_option(OPT["HALO"], 0)
     return _lib
+
+
+# selunet_option keys (include/selunet.h)
+OPT = {name: i for i, name in enumerate([
+    "HALO", "HALO_PERSIST", "WINO", "WINO_WGRAD", "WINO_WGRAD_TW", "WINO_WGRAD_WAVES", "WGRAD_WGS",
+    "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID"])}
+# environment variables the host maps onto options at load (A/B and ablation runs of tools/ and the
+# exact-fp32 comparison paths of the tests); SELUNET_NO_HALO=1 means HALO=0
+ENV_OPTIONS = {f"SELUNET_{k}": v for k, v in OPT.items() if k != "HALO"}
+
+
+def set_option(name: str, value: int) -> int:
+    """selunet_set_option by name (OPT); value < 0 restores the default. Returns the previous value."""
+    return int(load().selunet_set_option(OPT[name], int(value)))
 
 
 class SelunetError(RuntimeError):

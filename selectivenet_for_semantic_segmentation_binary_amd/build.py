@@ -4,10 +4,16 @@
 
 Objects are compiled in parallel and linked into `selectivenet_for_semantic_segmentation_binary_amd/libselunet.so`,
 next to this file, so the built library travels with the repository snapshot to the GPU box.
+
+Rebuilds are decided by content, not timestamps: each object carries a stamp holding the SHA-256 of
+its source, every header and the compiler flags, and the library embeds the fingerprint of the whole
+source set (`selunet_build_id()`), which `_lib.load()` compares with the sources next to it — a
+library built from other sources than the tree it is loaded from is refused.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -16,6 +22,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libselunet.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "selunet.h")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SELUNET_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
@@ -26,36 +33,75 @@ def _sources():
     return sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
-def _headers_mtime():
-    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hs.append(os.path.join(os.path.dirname(PKG), "include", "selunet.h"))
-    return max(os.path.getmtime(h) for h in hs if os.path.exists(h))
+def _headers():
+    hs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    return hs + [HEADER]
 
 
-def _compile(src, force):
-    obj = os.path.join(BUILD, src.replace(".hip", ".o"))
-    path = os.path.join(CSRC, src)
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(path), _headers_mtime()):
+def _digest(paths, extra=()):
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    for e in extra:
+        h.update(e.encode() + b"\0")
+    return h.hexdigest()
+
+
+def source_fingerprint() -> str:
+    """SHA-256 (first 24 hex digits) over every kernel source, header and the compiler flags."""
+    return _digest([os.path.join(CSRC, s) for s in _sources()] + _headers(), FLAGS)[:24]
+
+
+def _stamp_ok(stamp, want):
+    try:
+        with open(stamp) as f:
+            return f.read().strip() == want
+    except OSError:
+        return False
+
+
+def _compile(path, obj, want, force):
+    stamp = obj + ".sha"
+    if not force and os.path.exists(obj) and _stamp_ok(stamp, want):
         return obj
     cmd = [HIPCC, *FLAGS, "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+        raise RuntimeError(f"hipcc failed for {os.path.basename(path)}:\n{r.stderr[-6000:]}")
+    with open(stamp, "w") as f:
+        f.write(want)
     return obj
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+    heads = _headers()
+    fp = source_fingerprint()
+    # the build id: a one-line translation unit generated from the fingerprint
+    bid_src = os.path.join(BUILD, "build_id.hip")
+    bid = f'extern "C" const char* selunet_build_id(void) {{ return "{fp}"; }}\n'
+    if not os.path.exists(bid_src) or open(bid_src).read() != bid:
+        with open(bid_src, "w") as f:
+            f.write(bid)
+    jobs = [(os.path.join(CSRC, s), os.path.join(BUILD, s.replace(".hip", ".o")),
+             _digest([os.path.join(CSRC, s)] + heads, FLAGS)) for s in srcs]
+    jobs.append((bid_src, os.path.join(BUILD, "build_id.o"), _digest([bid_src], FLAGS)))
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+        objs = list(ex.map(lambda j: _compile(*j, force), jobs))
+    lib_stamp = LIB + ".sha"
+    if force or not os.path.exists(LIB) or not _stamp_ok(lib_stamp, fp):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        with open(lib_stamp, "w") as f:
+            f.write(fp)
     if verbose:
-        print(f"built {LIB}")
+        print(f"built {LIB} (sources {fp})")
     return LIB
 
 

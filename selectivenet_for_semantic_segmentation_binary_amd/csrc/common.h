@@ -31,6 +31,12 @@ int check_launch(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ------------------------------------------------------------------ options (host)
+// Kernel-selection and tuning options (selunet_option in selunet.h), set only through
+// selunet_set_option: the library reads no environment variables. Values < 0 mean "default".
+extern int64_t g_options[SELUNET_OPT_COUNT];
+inline int64_t option(int key, int64_t dflt) { return g_options[key] < 0 ? dflt : g_options[key]; }
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ------------------------------------------------------------------ element access

@@ -1962,29 +1962,16 @@ conv3x3_wgrad_wino_f32_kernel(GatherArg P, GatherArg Q, int co_tiles, int ci_chu
 }
 
 bool conv3x3_wgrad_wino_eligible(const GatherArg& p, const GatherArg& q, int dtype) {
-  static const bool on = [] {
-    const char* v = getenv("SELUNET_WINO_WGRAD");
-    return !(v && v[0] == '0');
-  }();
-  return on && dtype == SELUNET_F32 && conv3x3_wgrad_halo_eligible(p, q, dtype) && q.w % 2 == 0;
+  return option(SELUNET_OPT_WINO_WGRAD, 1) != 0 && dtype == SELUNET_F32 && conv3x3_wgrad_halo_eligible(p, q, dtype) && q.w % 2 == 0;
 }
 
 // splits of the Winograd weight gradient (64 x 64 tiles): ~256 workgroups over (co tile, ci chunk, split)
-static int wino_wgrad_tw() {
-  static const int tw = [] {
-    const char* v = getenv("SELUNET_WINO_WGRAD_TW");
-    return v && atoi(v) == 8 ? 8 : 16;
-  }();
-  return tw;
-}
+static int wino_wgrad_tw() { return option(SELUNET_OPT_WINO_WGRAD_TW, 16) == 8 ? 8 : 16; }
 
 int64_t conv3x3_wgrad_wino_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
   const int co_tiles = p.K / 64, ci_chunks = q.Ctot / 64;
   const int64_t total = (int64_t)q.n * cdiv(q.w, wino_wgrad_tw()) * cdiv(q.h, FTH);
-  static const int64_t target = [] {
-    const char* e = getenv("SELUNET_WGRAD_WGS");
-    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
-  }();
+  const int64_t target = std::max<int64_t>(1, option(SELUNET_OPT_WGRAD_WGS, 256));
   const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
   const int64_t per = cdiv(total, std::min(total, want));
   if (per_out) *per_out = per;
@@ -1999,10 +1986,7 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
   int64_t per;
   const int64_t splits = conv3x3_wgrad_wino_splits(p, q, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
-  static const int nw = [] {
-    const char* v = getenv("SELUNET_WINO_WGRAD_WAVES");
-    return v && atoi(v) == 8 ? 8 : 12;
-  }();
+  const int nw = option(SELUNET_OPT_WINO_WGRAD_WAVES, 12) == 8 ? 8 : 12;
   auto kern = tw == 8 ? (nw == 8 ? conv3x3_wgrad_wino_f32_kernel<8, 8> : conv3x3_wgrad_wino_f32_kernel<8, 12>)
                       : (nw == 8 ? conv3x3_wgrad_wino_f32_kernel<16, 8> : conv3x3_wgrad_wino_f32_kernel<16, 12>);
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(nw * 64), 0, st, p, q, co_tiles, ci_chunks, per, tiles_x, tiles_y,
@@ -2015,10 +1999,7 @@ int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t*
   const int bi = p.K % 128 == 0 ? 128 : 64;
   const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
   const int64_t total = (int64_t)q.n * cdiv(q.w, XTW) * cdiv(q.h, XTH);
-  static const int64_t target = [] {
-    const char* e = getenv("SELUNET_X2_WGRAD_WGS");
-    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
-  }();
+  const int64_t target = std::max<int64_t>(1, option(SELUNET_OPT_X2_WGRAD_WGS, 256));
   const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
   const int64_t per = cdiv(total, std::min(total, want));
   if (per_out) *per_out = per;
@@ -2066,10 +2047,7 @@ int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int dt
   // partials for the fixed-order reduction to read. One workgroup per CU (256) measured best:
   // 6.53 vs 6.94 ms/step at 16 images/GPU (512: two per CU, twice the partials), 11.8 vs 12.2 at
   // 32, equal at 128; 128 and 384 lose (SELUNET_WGRAD_WGS overrides)
-  static const int64_t target = [] {
-    const char* e = getenv("SELUNET_WGRAD_WGS");
-    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)256;
-  }();
+  const int64_t target = std::max<int64_t>(1, option(SELUNET_OPT_WGRAD_WGS, 256));
   const int64_t want = std::max<int64_t>(1, cdiv(target, (int64_t)co_tiles * ci_chunks));
   const int64_t per = cdiv(total, std::min(total, want));
   if (per_out) *per_out = per;
@@ -2125,13 +2103,7 @@ int64_t conv3x3_halo_tiles(const GatherArg& g) {
 constexpr int PERSIST_WGS_DEFAULT = 256;
 static int PERSIST_WGS = PERSIST_WGS_DEFAULT;  // selunet_set_halo_workgroups
 
-static bool persist_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("SELUNET_HALO_PERSIST");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+static bool persist_enabled() { return option(SELUNET_OPT_HALO_PERSIST, 1) != 0; }
 
 static bool halo_one_chunk(const GatherArg& g, int dtype) { return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64); }
 
@@ -2169,13 +2141,7 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
                      ep, n_tiles, tiles_x, tiles_y);
 }
 
-static bool wino_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("SELUNET_WINO");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+static bool wino_enabled() { return option(SELUNET_OPT_WINO, 1) != 0; }
 
 bool conv3x3_wino_shape_ok(int h, int w, int c_in, int c_src0, int n_cols) {
   return wino_enabled() && persist_enabled() && h >= TH && w >= TW && w % 2 == 0 && c_in % 32 == 0 &&

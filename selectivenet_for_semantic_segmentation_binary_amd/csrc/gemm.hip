@@ -919,11 +919,7 @@ static int64_t wgrad_splits(int64_t M, int tiles, int64_t* mchunk_out, int64_t w
   // workgroup target over (tile, pixel split): 512 (two per CU) measured 6.43 vs 6.57 ms/step at
   // 16 images/GPU against 2048 (fewer split partials to reduce), equal at 128; 256 and 1024 in
   // between (SELUNET_GEMM_WGRAD_WGS overrides); wgs: a kernel's own target (one workgroup per CU)
-  static const int64_t target_env = [] {
-    const char* e = getenv("SELUNET_GEMM_WGRAD_WGS");
-    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)512;
-  }();
-  const int64_t target = wgs > 0 ? wgs : target_env;
+  const int64_t target = wgs > 0 ? wgs : std::max<int64_t>(1, option(SELUNET_OPT_GEMM_WGRAD_WGS, 512));
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), cdiv(target, tiles)));
   const int64_t mchunk = cdiv(cdiv(M, splits), 64) * 64;
   if (mchunk_out) *mchunk_out = mchunk;
@@ -941,16 +937,8 @@ static void launch_gather(const GatherArg& g, const void* b, int N, int k_pad, c
 
 // Resident gather-GEMM workgroups the persistent launch aims for (2 per CU; a constant, not the
 // device's CU count, so slab rows never depend on the device); 0 = one tile per workgroup.
-// SELUNET_GATHER_WGS (profiling) or selunet_set_gather_workgroups (tests) override it.
-static int64_t gather_wgs_default() {
-  static const int64_t v = [] {
-    const char* e = getenv("SELUNET_GATHER_WGS");
-    return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)512;
-  }();
-  return v;
-}
-int64_t GATHER_WGS = -1;  // < 0: default
-static int64_t gather_wgs() { return GATHER_WGS < 0 ? gather_wgs_default() : GATHER_WGS; }
+// SELUNET_OPT_GATHER_WGS (selunet_set_option) or selunet_set_gather_workgroups (tests) override it.
+static int64_t gather_wgs() { return option(SELUNET_OPT_GATHER_WGS, 512); }
 
 // Row-tile workgroups (= statistics slab rows) of the gather GEMM for N output columns; independent
 // of the column tile width (64 or 128) so the caller can size slabs from (operand, N) alone.
@@ -995,17 +983,11 @@ static void launch_wgrad_impl(const GatherArg& p, const GatherArg& q, float* out
 
 using namespace selunet;
 
-bool selunet::halo_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("SELUNET_NO_HALO");
-    return !(v && v[0] == '1');
-  }();
-  return on;
-}
+bool selunet::halo_enabled() { return option(SELUNET_OPT_HALO, 1) != 0; }
 
 extern "C" int32_t selunet_set_gather_workgroups(int32_t wgs) {
   const int32_t prev = (int32_t)selunet::gather_wgs();
-  selunet::GATHER_WGS = wgs < 0 ? -1 : wgs;
+  g_options[SELUNET_OPT_GATHER_WGS] = wgs < 0 ? -1 : wgs;
   return prev;
 }
 

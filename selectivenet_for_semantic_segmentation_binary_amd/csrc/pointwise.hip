@@ -9,8 +9,11 @@
 
 namespace selunet {
 
-// ------------------------------------------------------------------ error state
+// ------------------------------------------------------------------ error state, options
 static thread_local char g_err[512] = "";
+
+int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(SELUNET_OPT_COUNT == 13, "g_options initialiser");
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -406,7 +409,9 @@ __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const B
     const double d = mean - (a.center ? (double)a.center[c] : 0.0);
     a.uvar_flag_o[c] = d * d <= (double)a.flag_ratio * var ? (float)(var * (double)a.count / (double)(a.count - 1)) : -1.0f;
   }
-  if (a.training && a.center_next_o) a.center_next_o[c] = (float)mean;
+  // a non-finite batch mean is not carried into the next step's center (it would poison every later
+  // shifted sum of this plan): the center falls back to 0, the unshifted statistics
+  if (a.training && a.center_next_o) a.center_next_o[c] = isfinite(mean) ? (float)mean : 0.0f;
   const double inv = 1.0 / sqrt(var + (double)a.eps);
   const double sc = (double)a.gamma[c] * inv;
   a.mean_o[c] = (float)mean;
@@ -512,33 +517,31 @@ __global__ void __launch_bounds__(1024) reduce_finalize_kernel(const S* __restri
   for (int s = 0; s < SETS; ++s) red[s][lane][cl] = acc[s];
   __syncthreads();
   if (SETS == 2 && fa.nbt && threadIdx.x == 0 && blockIdx.x == 0) *fa.nbt += 1;
-  if (lane != 0 || c >= C) return;
-  double t[SETS];
+  if (lane != 0) return;  // (wave-uniform: wave 0 stays whole for the wave-wide range-word max below)
+  float bound = 0.0f;      // lanes c >= C contribute 0
+  if (c < C) {
+    double t[SETS];
 #pragma unroll
-  for (int s = 0; s < SETS; ++s) {
-    double x = 0.0;
+    for (int s = 0; s < SETS; ++s) {
+      double x = 0.0;
 #pragma unroll
-    for (int l = 0; l < RF_LANES; ++l) x += red[s][l][cl];
-    t[s] = x;
-    if (sums_out) sums_out[s * C + c] = x;
+      for (int l = 0; l < RF_LANES; ++l) x += red[s][l][cl];
+      t[s] = x;
+      if (sums_out) sums_out[s * C + c] = x;
+    }
+    if constexpr (SETS == 2) {
+      bn_finalize_one(c, t[0], t[1], fa);
+      if (fa.bound_o) bound = (fabsf(fa.gamma[c]) * fa.bound_sq + fabsf(fa.beta[c])) * 1.0001f;
+    } else {
+      bn_bwd_finalize_one(c, C, t[0], t[1], t[2], ba);
+    }
   }
-  if constexpr (SETS == 2) {
-    bn_finalize_one(c, t[0], t[1], fa);
-    if (fa.bound_o) atomic_amax(fa.bound_o, (fabsf(fa.gamma[c]) * fa.bound_sq + fabsf(fa.beta[c])) * 1.0001f);
-  } else {
-    bn_bwd_finalize_one(c, C, t[0], t[1], t[2], ba);
-  }
+  if (SETS == 2 && fa.bound_o) atomic_amax(fa.bound_o, bound);
 }
 
 // rows up to which the fused reductions read the fp32 slab in one launch; above it a first level
 // (reduce_rows_l1) cuts the rows to <= RED_SPLITS fp64 split sums first (SELUNET_RF_SINGLE)
-static int64_t rf_single_rows() {
-  static const int64_t v = [] {
-    const char* e = getenv("SELUNET_RF_SINGLE");
-    return e ? (int64_t)atoll(e) : (int64_t)1024;
-  }();
-  return v;
-}
+static int64_t rf_single_rows() { return option(SELUNET_OPT_RF_SINGLE, 1024); }
 
 // slab [rows][SETS][c] fp32 -> launches of the fused reduce + finalize (ws: >= selunet_reduce_ws_bytes(SETS*c))
 template <int SETS>
@@ -1315,6 +1318,16 @@ extern "C" {
 const char* selunet_last_error(void) { return g_err; }
 int32_t selunet_version(void) { return 1; }
 
+int64_t selunet_set_option(int32_t key, int64_t value) {
+  if (key < 0 || key >= SELUNET_OPT_COUNT) {
+    set_error("selunet_set_option: unknown key %d", key);
+    return INT64_MIN;
+  }
+  const int64_t prev = g_options[key];
+  g_options[key] = value < 0 ? -1 : value;
+  return prev;
+}
+
 int selunet_pack_conv3x3(const float* w, int32_t co, int32_t ci, int32_t k_pad, void* fwd, void* dgrad,
                          int32_t dtype, void* stream) {
   SELUNET_REQUIRE(w && fwd && co > 0 && ci > 0 && k_pad >= 9 * ci, "pack_conv3x3: bad arguments");
@@ -1622,8 +1635,8 @@ int selunet_bn_bwd_apply_amax(const void* dz, const void* y, int64_t m, int32_t 
   SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
                   "bn_bwd_apply: bad arguments");
   SELUNET_REQUIRE(ok_channels(c), "bn_bwd_apply: C must be 64, 128, 256 or 512 (got %d)", c);
-  static const int u8 = [] { const char* v = getenv("SELUNET_APPLY_U"); return v && v[0] == '8'; }();
-  static const int64_t gcap = [] { const char* v = getenv("SELUNET_APPLY_GRID"); return v ? atoll(v) : 1024LL; }();
+  const bool u8 = option(SELUNET_OPT_APPLY_U8, 0) != 0;
+  const int64_t gcap = std::max<int64_t>(1, option(SELUNET_OPT_APPLY_GRID, 1024));
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), gcap));
   if (u8) {
     DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(blocks), dim3(TPB), 0, as_stream(stream),

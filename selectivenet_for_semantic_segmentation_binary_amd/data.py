@@ -109,16 +109,27 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
     fi, fl = os.path.join(cdir, f"{key}_images.npy"), os.path.join(cdir, f"{key}_labels.npy")
     ids = [a.split("_input")[0] for a, _ in pairs]
     shared = cache and parallel.is_initialized() and parallel.world_size() > 1
+    failed = os.path.join(cdir, f"{key}_FAILED")
     if shared and parallel.rank() != 0:
-        _wait_for_files((fi, fl), CACHE_WAIT_S)  # rank 0 writes (or has written) the cache
+        # rank 0 writes (or has written) the cache, or leaves the failure marker
+        _wait_for_files((fi, fl), CACHE_WAIT_S, failed=failed)
         return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     if cache and os.path.exists(fi) and os.path.exists(fl):
         return PatchSet(np.load(fi, mmap_mode="r"), np.load(fl, mmap_mode="r"), ids)
     imgs = np.empty((len(pairs), patch_size, patch_size, 3), np.uint8)
     labs = np.empty((len(pairs), patch_size, patch_size), np.uint8)
-    for i, (a, b) in enumerate(pairs):
-        imgs[i] = np.array(Image.open(os.path.join(root, a)).convert("RGB"))
-        labs[i] = np.array(Image.open(os.path.join(root, b)).convert("L"))
+    if shared and os.path.exists(failed):
+        os.remove(failed)
+    try:
+        for i, (a, b) in enumerate(pairs):
+            imgs[i] = np.array(Image.open(os.path.join(root, a)).convert("RGB"))
+            labs[i] = np.array(Image.open(os.path.join(root, b)).convert("L"))
+    except Exception as e:
+        if shared:  # the waiting ranks stop at once instead of polling until CACHE_WAIT_S
+            os.makedirs(cdir, exist_ok=True)
+            with open(failed, "w") as f:
+                f.write(f"rank 0 failed to decode the patch list: {e!r}\n")
+        raise
     if cache:
         os.makedirs(cdir, exist_ok=True)
         for path, arr in ((fi, imgs), (fl, labs)):
@@ -131,12 +142,16 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
 CACHE_WAIT_S = float(os.environ.get("SELUNET_CACHE_WAIT_S", 6 * 3600))
 
 
-def _wait_for_files(paths, limit_s, poll_s=0.5):
-    """Block until every path exists (they appear atomically, os.replace) or limit_s passes."""
+def _wait_for_files(paths, limit_s, poll_s=0.5, failed=None):
+    """Block until every path exists (they appear atomically, os.replace) or limit_s passes; raise
+    as soon as the `failed` marker (written by the rank that was to produce them) appears."""
     import time
 
     t0 = time.monotonic()
     while not all(os.path.exists(p) for p in paths):
+        if failed is not None and os.path.exists(failed):
+            with open(failed) as f:
+                raise RuntimeError(f.read().strip())
         if time.monotonic() - t0 > limit_s:
             raise TimeoutError(f"rank 0 did not write the patch cache within {limit_s:.0f} s: {paths}")
         time.sleep(poll_s)

@@ -163,8 +163,13 @@ def mask_flips(d, pre, head, logits, tol):
 
     Returns (flips, near0): the number of pixels whose mask bit differs from the reference's, and
     the number of reference logits within 1e-6 of the decision boundary. Needs the fixture's full
-    logits or its packed mask bits (`<head>_mask_bits`); every flipped pixel must lie within the
-    logit tolerance `tol` (relative to the reference's max |logit|) of the boundary."""
+    logits or its packed mask bits (`<head>_mask_bits`, with the sampled logits `<head>_idx/_val`).
+    A flip is accepted only where the reference logit lies within the logit error this run measures
+    on the same fixture: with full logits, |ref| at every flipped pixel <= the largest |ours - ref| over
+    the pixels that did not flip; with packed bits, |ours| at every flipped pixel (>= |ref| - error
+    there, and for a flip |ours| <= |ours - ref|) <= twice the largest |ours - ref| over the fixture's
+    logit samples (16384 of 8.4M pixels at batch 128, so their maximum sits in the error tail but
+    not necessarily at its end). `tol` (relative to the reference's max |logit|) caps both."""
     from oracle import unet_b_cpu as O  # (test infrastructure: the checker's threshold rule)
 
     logits = np.asarray(logits, np.float32)
@@ -174,16 +179,22 @@ def mask_flips(d, pre, head, logits, tol):
         ref = O.train_pred_mask(ref_logits).ravel()
         near0 = int((np.abs(ref_logits) < 1e-6).sum())
         absmax = float(np.abs(ref_logits).max())
-        at = np.abs(ref_logits.ravel())
+        diff = ours != ref
+        err = np.abs(logits.ravel().astype(np.float64) - ref_logits.ravel())
+        e_meas = float(err[~diff].max(initial=0.0))
+        at, bound = np.abs(ref_logits.ravel()), e_meas
     else:
         ref = np.unpackbits(d[pre + head + "_mask_bits"])[:ours.size]
         near0 = int(d[pre + head + "_near0_count"])
         absmax = float(d[pre + head + "_absmax"])
-        at = np.abs(logits.ravel()) + tol * absmax  # |ref| <= |ours| + logit error
-    diff = ours != ref
+        diff = ours != ref
+        idx = d[pre + head + "_idx"]
+        e_meas = float(np.abs(logits.ravel()[idx].astype(np.float64) - d[pre + head + "_val"]).max())
+        at, bound = np.abs(logits.ravel()), 2.0 * e_meas
     flips = int(diff.sum())
     if flips:
-        assert at[diff].max() <= 2 * tol * absmax, (head, flips, float(at[diff].max()), absmax)
+        worst = float(at[diff].max())
+        assert worst <= min(bound, tol * absmax), (head, flips, worst, "measured logit error", e_meas, absmax)
     return flips, near0
 
 

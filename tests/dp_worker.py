@@ -43,7 +43,8 @@ def main(fname, out, backend="gloo"):
         loss = aux_loss + select_loss
         opt.zero_grad()
         loss.backward()
-        res = {"loss": loss.item(), "coverage": coverage.item(), "aux_loss": aux_loss.item(),
+        res = {"world": torch.distributed.get_world_size(), "backend": torch.distributed.get_backend(),
+               "loss": loss.item(), "coverage": coverage.item(), "aux_loss": aux_loss.item(),
                "select_loss": select_loss.item(), "output": o.detach().cpu().numpy(),
                "selection": sel.detach().cpu().numpy(), "aux": aux.detach().cpu().numpy()}
         if rank == 0:

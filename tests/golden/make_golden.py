@@ -790,6 +790,95 @@ def augment_bf16ref(fname):
     print(f"wrote {path}: reference bf16-autocast step, loss {loss.item():.6f} (fp32 {float(d['s0/loss']):.6f})")
 
 
+class _Absent(type(sys)):
+    """sys.modules placeholder for a module the reference imports at top level but whose functions
+    the recorded path never calls (cv2, skimage.color, torchvision.transforms: the RGB input path
+    of utils/data_utils.py uses none of them). Any attribute use raises, so a call would fail loudly
+    instead of running a stand-in."""
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        raise RuntimeError(f"{self.__name__}.{name} is absent in this container: the recorded path must not use it")
+
+
+def _import_ref_data_utils():
+    """The reference's own utils/data_utils.py, freshly imported (its module-level np.random.seed(42),
+    :48, runs again), with placeholders for the three absent top-level imports (:2,4,8)."""
+    import importlib
+    saved = {k: sys.modules.get(k) for k in ("cv2", "skimage", "skimage.color", "torchvision",
+                                             "torchvision.transforms", "data_utils")}
+    sk, tv = _Absent("skimage"), _Absent("torchvision")
+    sk.__dict__["color"] = sys.modules["skimage.color"] = _Absent("skimage.color")
+    tv.__dict__["transforms"] = sys.modules["torchvision.transforms"] = _Absent("torchvision.transforms")
+    sys.modules.update({"cv2": _Absent("cv2"), "skimage": sk, "torchvision": tv})
+    sys.modules.pop("data_utils", None)
+    try:
+        return importlib.import_module("data_utils")
+    finally:
+        for k, v in saved.items():
+            if k == "data_utils":
+                continue
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+
+
+def data_fixture(fname="data_rgb_n30_32.npz", per_fold=6, size=32):
+    """The RGB data path recorded from the reference's own utils/data_utils.py (:48-86, 94-168,
+    174-236) on the patch directory tests/_patchdir.py writes: the fold split lists of
+    construct_train_valid / construct_test for every test fold (each in a fresh import, as each
+    train.py / eval.py process is), and PatchDataset.__getitem__ followed by the training transform
+    (Normalization, RandomFlip, ToTensor: train.py:367) and the validation transform (Normalization,
+    ToTensor: train.py:368, eval.py:92) — composed by calling them in order, as transforms.Compose
+    does — for every item of fold 2's lists. np.random is re-seeded per item and the two draws
+    RandomFlip consumes are recorded as flip bits (1: fliplr, 2: flipud). The JPEG/PNG files are
+    identified by SHA-1 so a regenerated directory can be checked to hold the same bytes."""
+    import tempfile
+    sys.path.insert(0, REPO)
+    from tests._patchdir import make_patch_dir
+
+    out = {"meta_per_fold": per_fold, "meta_size": size, "meta_mag": 200}
+    with tempfile.TemporaryDirectory() as root:
+        make_patch_dir(root, per_fold=per_fold, size=size)
+        sub = os.path.join(root, f"200x_{size}")
+        names = sorted(os.listdir(sub))
+        out["files"] = np.array(names)
+        out["files_sha1"] = np.array([hashlib.sha1(open(os.path.join(sub, f), "rb").read()).hexdigest() for f in names])
+        for fold in (1, 2, 3, 4, 5):
+            du = _import_ref_data_utils()
+            tr, va = du.construct_train_valid(root, test_fold=fold)
+            out[f"fold{fold}/train"], out[f"fold{fold}/valid"] = tr.astype(str), va.astype(str)
+            out[f"fold{fold}/test"] = du.construct_test(root, test_fold=fold).astype(str)
+        du = _import_ref_data_utils()
+        tr, va = out["fold2/train"], out["fold2/valid"]
+        for split, lst, train in (("train", tr, True), ("valid", va, False)):
+            ds = du.PatchDataset(root, lst, 200, size, "RGB", transform=None)
+            xs, ts, fl, ids = [], [], [], []
+            for i in range(len(ds)):
+                np.random.seed(500 + i)
+                r = np.random.rand(2) if train else np.zeros(2)
+                np.random.seed(500 + i)
+                data = ds[i]
+                data = du.Normalization(mean=0.5, std=0.5)(data)
+                if train:
+                    data = du.RandomFlip()(data)
+                data = du.ToTensor()(data)
+                xs.append(data["input"].numpy())
+                ts.append(data["label"].numpy())
+                fl.append(int(r[0] > 0.5) | (int(r[1] > 0.5) << 1))
+                ids.append(data["id"])
+            out[f"{split}/input"] = np.stack(xs)
+            out[f"{split}/label"] = np.stack(ts)
+            out[f"{split}/flips"] = np.array(fl, np.uint8)
+            out[f"{split}/ids"] = np.array(ids)
+    path = os.path.join(HERE, fname)
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}: {len(names)} files, fold-2 train {len(tr)} / valid {len(va)} items, "
+          f"train flips {np.bincount(out['train/flips'], minlength=4).tolist()}")
+
+
 def check_checkpointing(n=2, size=32):
     """The checkpointed reference step equals the plain one (same modules, same arithmetic)."""
     x, lab = make_batch(n, size, seed=1)
@@ -847,6 +936,18 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["dp2"]:
         step_fixture("dp_sel_n8_32_c2.npz", 8, 32, selective=True, lamb=2, steps=2, chunks=2)
         sys.exit(0)
+    if sys.argv[1:] == ["dp8"]:  # train.sh:1 runs 8 device ids: DataParallel over 8 replicas
+        step_fixture("dp_sel_n16_32_c8.npz", 16, 32, selective=True, lamb=2, steps=2, chunks=8)
+        augment_ensemble("dp_sel_n16_32_c8.npz", k_members=8)
+        augment_conv_noise("dp_sel_n16_32_c8.npz", k_members=16)
+        sys.exit(0)
+    if sys.argv[1:] == ["nosel128"]:  # BASELINE configs[1]: UNet_B --selective 0 at batch 128, 256x256
+        f = "step_nosel_n128_256.npz"
+        step_fixture(f, 128, 256, selective=False, steps=1, full_outputs=False, fp64=False, ckpt=True,
+                     out_samples=16384, mask_bits=True, data_seed=0)
+        augment_bf16ref(f)
+        augment_ensemble(f, k_members=int(os.environ.get("ENS_MEMBERS", 3)), ckpt=True)
+        sys.exit(0)
     if sys.argv[1:] == ["miou"]:
         miou_fixture()
         sys.exit(0)
@@ -873,6 +974,9 @@ if __name__ == "__main__":
     if sys.argv[1:2] == ["bf16ref"]:
         for f in sys.argv[2:]:
             augment_bf16ref(f)
+        sys.exit(0)
+    if sys.argv[1:] == ["data"]:
+        data_fixture()
         sys.exit(0)
     if sys.argv[1:] == ["hard"]:
         hard_cases()

@@ -44,3 +44,48 @@ def test_transform_rules_on_known_values():
     x, t = OD.transform(im, lb, flips=3)  # fliplr then flipud (utils/data_utils.py:113-121)
     assert np.array_equal(t, lb[::-1, ::-1].astype(np.float32))
     assert np.array_equal(x, ((im[::-1, ::-1] - 0.5) / 0.5).transpose(2, 0, 1))
+
+
+# ----------------------------------------------------------------------------- reference fixture
+def _fixture_dir(tmp_path):
+    """The patch directory data_rgb_n30_32.npz was recorded on (tests/golden/make_golden.py data),
+    regenerated, with every file's bytes checked against the recorded SHA-1."""
+    import hashlib
+    import os
+
+    from tests import _golden as G
+    d = G.load("data_rgb_n30_32.npz")
+    root = make_patch_dir(str(tmp_path), per_fold=int(d["meta_per_fold"]), size=int(d["meta_size"]))
+    sub = os.path.join(root, f"200x_{int(d['meta_size'])}")
+    assert sorted(os.listdir(sub)) == [str(f) for f in d["files"]]
+    for f, h in zip(d["files"], d["files_sha1"]):
+        assert hashlib.sha1(open(os.path.join(sub, str(f)), "rb").read()).hexdigest() == str(h), f
+    return d, root
+
+
+def test_fold_splits_match_reference_fixture(tmp_path):
+    """construct_train_valid / construct_test of the host side and of the oracle against the lists the
+    reference's own utils/data_utils.py produced on the same directory (one fresh import per fold)."""
+    d, root = _fixture_dir(tmp_path)
+    for fold in (1, 2, 3, 4, 5):
+        tr, va = D.construct_train_valid(root, test_fold=fold)
+        otr, ova = OD.construct_train_valid(root, test_fold=fold)
+        for got in ((tr, va), (otr, ova)):
+            assert np.array_equal(got[0].astype(str), d[f"fold{fold}/train"]), fold
+            assert np.array_equal(got[1].astype(str), d[f"fold{fold}/valid"]), fold
+        assert np.array_equal(D.construct_test(root, test_fold=fold).astype(str), d[f"fold{fold}/test"])
+
+
+def test_oracle_items_match_reference_fixture(tmp_path):
+    """The oracle's PatchDataset.__getitem__ + Normalization [+ RandomFlip] + ToTensor restatement
+    against the reference's own outputs for every item of fold 2 (flip draws as recorded): inputs
+    bit-exact, labels equal (the reference's LongTensor values)."""
+    d, root = _fixture_dir(tmp_path)
+    for split, train in (("train", True), ("valid", False)):
+        lst = d[f"fold2/{split}"]
+        for i, (a, b) in enumerate(lst):
+            inp, lab, pid = OD.read_patch(root, str(a), str(b), 200, int(d["meta_size"]))
+            x, t = OD.transform(inp, lab, flips=int(d[f"{split}/flips"][i]), train=train)
+            assert np.array_equal(x.view(np.uint32), d[f"{split}/input"][i].view(np.uint32)), (split, i)
+            assert np.array_equal(t, d[f"{split}/label"][i].astype(np.float32)), (split, i)
+            assert pid == str(d[f"{split}/ids"][i])

@@ -65,3 +65,25 @@ def test_h_rgb_batches_match_restatement(tmp_path):
         assert tuple(x.shape) == xe.shape and xe.shape[1] == 3
         assert np.abs(x.cpu().numpy() - xe).max() <= 1e-5
         assert np.array_equal(t.cpu().numpy(), te)
+
+
+def test_prep_batch_matches_reference_fixture(tmp_path):
+    """The GPU expansion (data.decode_patch_list + selunet_prep_batch: /255, Normalization,
+    RandomFlip with the recorded draws, NCHW fp32, label truncation) against the reference's own
+    utils/data_utils.py outputs on the same files (tests/golden/data_rgb_n30_32.npz, recorded by
+    make_golden.py data): fold 2's training items with their flips and its validation items without;
+    inputs bit-exact, labels equal to the reference's LongTensor values."""
+    from tests.test_data_oracle import _fixture_dir
+
+    d, root = _fixture_dir(tmp_path)
+    size = int(d["meta_size"])
+    for split in ("train", "valid"):
+        lst = d[f"fold2/{split}"]
+        ps = D.decode_patch_list(root, lst, patch_mag=200, patch_size=size, cache=False)
+        imgs = torch.tensor(np.asarray(ps.images), device="cuda")
+        labs = torch.tensor(np.asarray(ps.labels), device="cuda")
+        flips = torch.tensor(d[f"{split}/flips"], device="cuda") if split == "train" else None
+        x, t = D.prep_batch(imgs, labs, flips)
+        assert np.array_equal(x.cpu().numpy().view(np.uint32), d[f"{split}/input"].view(np.uint32)), split
+        assert np.array_equal(t.cpu().numpy(), d[f"{split}/label"].astype(np.float32)), split
+        assert list(ps.ids) == [str(s) for s in d[f"{split}/ids"]]

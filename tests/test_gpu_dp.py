@@ -37,10 +37,14 @@ def _gpus():
 
 @pytest.mark.parametrize("fname,backend", [
     ("dp_sel_n8_32_c4.npz", "gloo"),
+    # the world size train.sh:1 runs (8 device ids), rehearsed with all 8 ranks on cuda:0
+    ("dp_sel_n16_32_c8.npz", "gloo"),
     pytest.param("dp_sel_n8_32_c2.npz", "nccl",
                  marks=pytest.mark.skipif(_gpus() < 2, reason="RCCL data parallelism needs >= 2 GPUs")),
     pytest.param("dp_sel_n8_32_c4.npz", "nccl",
                  marks=pytest.mark.skipif(_gpus() < 4, reason="RCCL data parallelism needs >= 4 GPUs")),
+    pytest.param("dp_sel_n16_32_c8.npz", "nccl",
+                 marks=pytest.mark.skipif(_gpus() < 8, reason="RCCL data parallelism needs >= 8 GPUs")),
 ])
 def test_multi_rank_dp_matches_dataparallel_fixture(fname, backend, tmp_path):
     d = G.load(fname)
@@ -49,7 +53,7 @@ def test_multi_rank_dp_matches_dataparallel_fixture(fname, backend, tmp_path):
     procs = []
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
-                   WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
+                   WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, "-m", "tests.dp_worker", fname, str(tmp_path), backend],
                                       cwd=REPO, env=env))
     codes = []
@@ -64,6 +68,8 @@ def test_multi_rank_dp_matches_dataparallel_fixture(fname, backend, tmp_path):
     fails = []
     for s in range(int(d["meta_steps"])):
         rs = [np.load(tmp_path / f"r{r}_s{s}.npz") for r in range(world)]
+        # each rank reports the group it ran in: size and backend as torch.distributed saw them
+        assert [(int(x["world"]), str(x["backend"])) for x in rs] == [(world, backend)] * world
         losses = {float(x["loss"]) for x in rs}
         assert len(losses) == 1, losses  # every rank computed the same global loss
         r0 = rs[0]

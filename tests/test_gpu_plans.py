@@ -9,9 +9,8 @@ over real Adam steps runs agree to fp32 rounding, not bit for bit: step-0 head o
 relative (nothing has been updated yet); later steps' outputs 1e-2 relative to the tensor max and
 parameters within 5e-3 absolute (Adam normalises the update, so an element whose gradient is
 rounding noise moves by up to +-lr per step either way — the same bound the reference-parity
-tests use for later steps). Losses: steps 0-1 within 1e-6 relative; step 2, after two such
-updates, 1e-4 (measured: recorded and replayed runs are each bit-reproducible, and differ at step 2
-by 4e-7 to 1e-5 relative depending on which elements' noise-level gradients flip sign).
+tests use for later steps). Losses: steps 0-1 within 1e-6 relative, step 2 within 1e-5, with the BN
+statistics unshifted on both paths.
 """
 import gc
 
@@ -47,14 +46,18 @@ def _run(plans, steps=3, n=2, size=64, seed=0, lr=1e-3, same_batch=False):
     return np.array(losses), snap, params, net
 
 
-def test_replayed_steps_match_recorded_steps():
+def test_replayed_steps_match_recorded_steps(monkeypatch):
+    # unshifted BN statistics (SELUNET_BN_SHIFT=0): with the default shift a replayed step centres its
+    # sums on the previous step's mean while the first recorded one uses 0, so the two paths would
+    # differ in statistics rounding by design (test_replay_with_bn_shift_matches_to_rounding covers it)
+    monkeypatch.setenv("SELUNET_BN_SHIFT", "0")
     l_on, o_on, p_on, net = _run(True)
     l_off, o_off, p_off, _ = _run(False)
     eng = net._engine()
     assert sum(len(v) for v in eng._plans.values()) >= 1 and all(e.plan is not None for v in eng._plans.values()
                                                                    for e in v)
     assert np.allclose(l_on[:2], l_off[:2], rtol=1e-6, atol=0), (l_on, l_off)
-    assert np.allclose(l_on[2:], l_off[2:], rtol=1e-4, atol=0), (l_on, l_off)
+    assert np.allclose(l_on[2:], l_off[2:], rtol=1e-5, atol=0), (l_on, l_off)
     assert np.abs(o_on[0] - o_off[0]).max() <= 1e-4 * max(1.0, np.abs(o_off[0]).max())
     for a, b in zip(o_on[1:], o_off[1:]):
         assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())

@@ -149,7 +149,8 @@ def _run_oracle_fixture(fname, loss_form="literal"):
 
 
 @pytest.mark.parametrize("fname", ["step_sel_n2_64.npz", "step_nosel_n2_64.npz",
-                                   "step_sel_lamb8_n3_32.npz", "dp_sel_n8_32_c4.npz"])
+                                   "step_sel_lamb8_n3_32.npz", "dp_sel_n8_32_c4.npz",
+                                   "dp_sel_n16_32_c8.npz"])
 def test_oracle_train_step_matches_reference(fname):
     _run_oracle_fixture(fname, loss_form="literal")
 

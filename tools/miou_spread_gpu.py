@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import selectivenet_for_semantic_segmentation_binary_amd as S  # noqa: E402
 import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics, mean_iou  # noqa: E402
-from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, make_patches_hard, preprocess  # noqa: E402
 
 
 def run(xtr, ltr, xva, lva, a, member):
@@ -70,16 +70,25 @@ def main():
     ap.add_argument("--lr-decay", type=float, default=0.0, help="multiply lr by this at half the epochs")
     ap.add_argument("--lamb", type=float, default=2)
     ap.add_argument("-k", type=int, default=8)
+    ap.add_argument("--hard", default="", help="';'-separated make_patches_hard settings "
+                    "'contrast,noise,texture,decoys' to sweep (empty: make_patches)")
     a = ap.parse_args()
-    xtr, ltr = preprocess(*make_patches(a.n_train, a.size, seed=2024))
-    xva, lva = preprocess(*make_patches(a.n_val, a.size, seed=2025))
-    res = [run(xtr, ltr, xva, lva, a, m) for m in range(a.k + 1)]
-    tr = np.array([r[0] for r in res])
-    va = np.array([r[1] for r in res])
-    print(f"cfg {vars(a)}")
-    print("train mIoU", np.round(tr, 5), "val mIoU", np.round(va, 5), "final loss", [round(r[2], 4) for r in res])
-    print(f"SPREAD train {np.abs(tr[1:] - tr[0]).max():.5f} val {np.abs(va[1:] - va[0]).max():.5f} "
-          f"val range {va.max() - va.min():.5f}", flush=True)
+    for cfg in (a.hard.split(";") if a.hard else [None]):
+        if cfg:
+            c, nz, tx, dc = (float(v) for v in cfg.split(","))
+            gen = lambda n, seed: make_patches_hard(n, a.size, seed=seed, contrast=c, noise=nz, texture=tx,  # noqa
+                                                    decoys=int(dc))
+        else:
+            gen = lambda n, seed: make_patches(n, a.size, seed=seed)  # noqa: E731
+        xtr, ltr = preprocess(*gen(a.n_train, 2024))
+        xva, lva = preprocess(*gen(a.n_val, 2025))
+        res = [run(xtr, ltr, xva, lva, a, m) for m in range(a.k + 1)]
+        tr = np.array([r[0] for r in res])
+        va = np.array([r[1] for r in res])
+        print(f"cfg {vars(a)} hard={cfg}")
+        print("train mIoU", np.round(tr, 5), "val mIoU", np.round(va, 5), "final loss", [round(r[2], 4) for r in res])
+        print(f"SPREAD hard={cfg} train {np.abs(tr[1:] - tr[0]).max():.5f} val {np.abs(va[1:] - va[0]).max():.5f} "
+              f"val range {va.max() - va.min():.5f} val0 {va[0]:.5f}", flush=True)
 
 
 if __name__ == "__main__":
