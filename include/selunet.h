@@ -54,6 +54,7 @@ enum {
   SELUNET_OPT_RF_SINGLE,          /* slab rows reduced in one launch by the fused reductions (1024) */
   SELUNET_OPT_APPLY_U8,           /* BN-backward apply: 8 channel groups per thread (0) */
   SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
+  SELUNET_OPT_WX2,                /* split-fp16 3x3 layers on the Winograd F(2,3) kernel where eligible (1) */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
@@ -210,6 +211,18 @@ int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, f
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
+/* The same fp32 3x3 conv forward / data gradient on split-fp16 operands as a 1-D Winograd F(2,3) along
+ * x (model.py:11): per kernel row dy and output pair (x, x+1), M_xi = sum_c U_xi[c] * V_xi[c] over
+ * V = (d0 - d2, d1 + d2, d2 - d1, d1 - d3) of the four inputs x-1..x+2 (formed in fp32 from the
+ * BN+ReLU-transformed source, then split) and U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2) of the kernel
+ * row (fp64, rounded once, then split); y(x) = (M0 + M1) + M2, y(x+1) = (M1 - M2) - M3. Four fp16
+ * products per output pair and kernel row instead of six: 2/3 of selunet_conv3x3_x2's MFMAs. w: a
+ * SELUNET_PACK_CONV3X3_WX2 pack. Same gathers, range words, epilogues and statistics slab rows as
+ * selunet_conv3x3_x2; selunet_conv3x3_wx2_ok tells whether a layer can take it (h, w >= 16, w even,
+ * C and c_src0 multiples of 16, C >= 64, n_cols a multiple of 128). */
+int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
+int selunet_conv3x3_wx2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
+                        const float* amax0, const float* amax1, void* stream);
 /* Range word of a training-mode BatchNorm+ReLU output relu(gamma*xhat + beta) over `count` values
  * per channel: |xhat| <= sqrt(count - 1) for batch statistics (Samuelson's inequality), so
  * *out = max_c |gamma_c| * sqrt(count) + max_c |beta_c| bounds every element (max-pooled copies
@@ -272,6 +285,13 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * matrix: fwd + co*9*ci (co floats), dgrad + ci*9*co (ci floats). ci, co multiples of 32. */
 /* SELUNET_PACK_CONVT_X2 (fp32): the same split-fp16 format for a ConvTranspose2d weight [ci][co][2][2]:
  * fwd = [4*co][ci] (row (a*2+b)*co + o, k_pad = ci) + 4*co unscale factors, dgrad = [ci][4*co] + ci. */
+/* SELUNET_PACK_CONV3X3_WX2 (fp32): split-fp16 Winograd operands of selunet_conv3x3_wx2, k_pad = 12*ci;
+ * fwd = [co][12*ci] and dgrad = [ci][12*co] 32-bit words (dgrad from the flipped / transposed kernel):
+ * the U values of row r (output channel o for fwd, input channel c for dgrad) over the k channels in
+ * blocks ((k / 16) * 3 + dy) * 4 + q of 16 channels (q = 0, 2, 1, 3 for xi = 0, 1, 2, 3), each block
+ * stored as 16 fp16 high parts then 16
+ * low parts, the row scaled by 2^e_row (max|U_row| * 2^e_row < 2^14); the row unscale factors follow
+ * the matrix as for SELUNET_PACK_CONV3X3_X2. ci, co multiples of 16, at most 512. */
 /* SELUNET_PACK_COPY (any dtype): co*ci fp32 values w -> fwd unchanged (dgrad unused) — the heads'
  * current weights and biases (model.py:62,65,66) gathered into the contiguous [heads][64] / [heads]
  * operands of selunet_heads_fwd in the same launch. */
@@ -281,7 +301,8 @@ enum {
   SELUNET_PACK_CONV3X3_WINO = 2,
   SELUNET_PACK_CONV3X3_X2 = 3,
   SELUNET_PACK_CONVT_X2 = 4,
-  SELUNET_PACK_COPY = 5
+  SELUNET_PACK_COPY = 5,
+  SELUNET_PACK_CONV3X3_WX2 = 6
 };
 typedef struct selunet_pack_desc {
   const float* w;

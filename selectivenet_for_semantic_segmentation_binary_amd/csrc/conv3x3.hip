@@ -2115,6 +2115,8 @@ static int persist_rows(const GatherArg& g, int N) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(pt, PERSIST_WGS / std::max(1, N / 128)));
 }
 
+int64_t conv3x3_persist_rows(const GatherArg& g, int N) { return persist_rows(g, N); }
+
 bool conv3x3_halo_persistent(const GatherArg& g, int dtype) { return !halo_one_chunk(g, dtype) && persist_enabled(); }
 
 int64_t conv3x3_halo_stats_rows(const GatherArg& g, int N, int dtype) {

@@ -466,6 +466,11 @@ int convt_dgrad_x2_launch(const GatherArg& g, const float* w, int N, const EpiAr
                           hipStream_t st);
 int convt_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                     hipStream_t st);
+// the same on the split-fp16 1-D Winograd F(2,3) kernel (conv3x3_wx2.hip, selunet_conv3x3_wx2)
+bool conv3x3_wx2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
+int conv3x3_wx2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                       const float* amax1, hipStream_t st);
+int64_t conv3x3_persist_rows(const GatherArg& g, int N);  // workgroup rows of the persistent 3x3 kernels
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,

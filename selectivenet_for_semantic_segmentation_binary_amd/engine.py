@@ -31,6 +31,11 @@ BN_CENTER_RATIO = None if os.environ.get("SELUNET_BN_TWOPASS", "0") == "1" else 
 FIRST_KPAD = 32  # packed K of encoder_layer_1_1 (9 * C_in <= 27), see selunet_first_conv_fwd
 
 
+# split-fp16 ("x2") kernel forms of a 3x3 layer: direct (selunet_conv3x3_x2) or Winograd F(2,3)
+# (selunet_conv3x3_wx2); both read and write the same operand range words
+X2_MODES = ("x2", "wx2")
+
+
 def _rup(a, b):
     return (a + b - 1) // b * b
 
@@ -250,9 +255,12 @@ class Engine:
             dg = None
             if self._x2_ok(name, ci, co, hw, need_dgrad, training):
                 mode, kpad, kind = "x2", 9 * ci, K.PACK_CONV3X3_X2
+                if self._shape_ok("selunet_conv3x3_wx2_ok", name, ci, co, hw, need_dgrad):
+                    # (forward and data gradient both on the split-fp16 Winograd F(2,3) kernel)
+                    mode, kpad, kind = "wx2", 12 * ci, K.PACK_CONV3X3_WX2
                 fwd = K.keep(torch.empty(co * kpad + co, dtype=torch.float32, device=dev))
                 if need_dgrad:
-                    dg = K.keep(torch.empty(ci * 9 * co + ci, dtype=torch.float32, device=dev))
+                    dg = K.keep(torch.empty(ci * (kpad // ci) * co + ci, dtype=torch.float32, device=dev))
             else:
                 if self._wino_ok(name, ci, co, hw, need_dgrad):
                     mode, kpad, taps, kind = "wino", 12 * ci, 12, K.PACK_CONV3X3_WINO
@@ -265,7 +273,7 @@ class Engine:
             pl.d[pl.n] = K.PackDesc(K.ptr(w), K.ptr(fwd), K.ptr(dg), kind, co, ci, kpad, 0)
             pl.n += 1
             packs[name] = WPack(fwd, dg, kpad, co, mode)
-        x2 = any(wp.mode == "x2" for wp in packs.values())
+        x2 = any(wp.mode in X2_MODES for wp in packs.values())
         for name, ci, co in LY.UNPOOLS:
             w = P[f"{name}.weight"]
             if x2:  # ConvTranspose2d forward / data gradient on split-fp16 operands (selunet_gemm_gather_x2)
@@ -302,12 +310,12 @@ class Engine:
         """A 3x3 conv (forward or data gradient) through the direct halo / gather kernels, or the
         fp32 Winograd / split-fp16 kernel when the layer's operands were packed for it (srcs: the
         gather's sources, whose range words the split-fp16 kernel reads)."""
-        if mode == "x2":
+        if mode in X2_MODES:
             words = [s.amax for s in srcs]
             if any(wd is None for wd in words):
                 raise RuntimeError("split-fp16 conv: a source without its range word")
-            K.call("selunet_conv3x3_x2", g, K.ptr(b), n_cols, ep, K.ptr(words[0]),
-                   K.ptr(words[1]) if len(words) > 1 else None, self.stream)
+            K.call("selunet_conv3x3_wx2" if mode == "wx2" else "selunet_conv3x3_x2", g, K.ptr(b), n_cols, ep,
+                   K.ptr(words[0]), K.ptr(words[1]) if len(words) > 1 else None, self.stream)
         elif mode == "wino":
             K.call("selunet_conv3x3_wino", g, K.ptr(b), n_cols, ep, self.stream)
         else:
@@ -498,7 +506,7 @@ class Engine:
         ctx.wpack = self.pack_weights(P, need_dgrad=training and need_backward, hw=(H, W), training=training,
                                       heads=heads)
         hw, hb = ctx.wpack.pop("heads")
-        ctx.x2 = any(wp.mode == "x2" for wp in ctx.wpack.values())
+        ctx.x2 = any(wp.mode in X2_MODES for wp in ctx.wpack.values())
         if ctx.x2:  # the operand range words of this step, zeroed for their atomic-max producers
             keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy", "du")]
             keys += ["up:" + nm for nm, _, _ in LY.UNPOOLS]
@@ -597,7 +605,7 @@ class Engine:
             return None
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         wp = ctx.wpack[name]
-        dyw = self._word(ctx, "dy:" + name) if wp.mode == "x2" else None
+        dyw = self._word(ctx, "dy:" + name) if wp.mode in X2_MODES else None
         if dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
             K.call("selunet_bn_bwd_apply_amax", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                    K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.code, self.stream)
