@@ -219,7 +219,7 @@ const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t
  * products per output pair and kernel row instead of six: 2/3 of selunet_conv3x3_x2's MFMAs. w: a
  * SELUNET_PACK_CONV3X3_WX2 pack. Same gathers, range words, epilogues and statistics slab rows as
  * selunet_conv3x3_x2; selunet_conv3x3_wx2_ok tells whether a layer can take it (h, w >= 16, w even,
- * C and c_src0 multiples of 16, C >= 64, n_cols a multiple of 128). */
+ * C and c_src0 multiples of 16, C >= 64, n_cols a multiple of 64). */
 int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
 int selunet_conv3x3_wx2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                         const float* amax0, const float* amax1, void* stream);

@@ -14,8 +14,9 @@
 // Workgroup: 512 threads, one per CU, persistent over the output tiles prow, prow + gp, ... of one
 // BN-column tile (as the direct kernel: statistics in registers, one slab row per workgroup). Tile
 // 16 x 16 px = 128 output pairs. The 8 waves split plane groups x pairs x columns: wave w holds the
-// accumulators of planes {0, 1} or {2, 3} (w & 1) for 64 pairs x 64 columns (BN = 128) — 2 planes x
-// 2 x 2 subtiles = 128 accumulator registers; the four planes of a pair meet in the LDS epilogue.
+// accumulators of planes {0, 1} or {2, 3} (w & 1) for 64 pairs x 64 columns at BN = 128 (2 planes x
+// 2 x 2 subtiles = 128 accumulator registers) or 32 pairs x 64 columns at BN = 64; the four planes
+// of a pair meet in the LDS epilogue.
 // A step is (kernel row dy, s): the waves of group wp multiply plane 2 wp + s, so a step stages the
 // weights of two planes (16 KiB) and each wave reads 8 fragments for 12 MFMAs (the direct kernel's
 // ratio); six steps per 16-channel chunk.
@@ -56,7 +57,7 @@ __global__ void __launch_bounds__(WX_THREADS, 1)
 conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiArg ep, int n_tiles, int tiles_x,
                    int tiles_y, int ptiles, int gp, const float* __restrict__ wcs, const float* __restrict__ amax0,
                    const float* __restrict__ amax1) {
-  static_assert(BN == 128, "128-column tiles");
+  static_assert(BN == 128 || BN == 64, "64- or 128-column tiles");
   constexpr int WN_ = BN / 64;                  // column-wave groups
   constexpr int WM_ = 4 / WN_;                  // pair-wave groups
   constexpr int MT = 4 / WM_;                   // 32-pair subtiles per wave (2 at BN = 128)
@@ -66,7 +67,12 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   static_assert(B_ROUNDS * 16 * WX_THREADS == BBUF, "weight rows split evenly over the threads");
   constexpr int OFF_B = 2 * WX_VBUF;
   constexpr int SMEM_EPI = WX_TH * WX_TW * (BN + 4) * 4;
-  constexpr int OFF_RAW = (OFF_B + 2 * BBUF > SMEM_EPI ? OFF_B + 2 * BBUF : SMEM_EPI);  // above the epilogue tile
+  // statistics registers: fp32 at BN = 128 (as the direct kernel: fp64 ones would not fit its registers),
+  // fp64 at BN = 64 (the full-resolution layers, ~128 tiles folded into each thread's sums)
+  using Acc = std::conditional_t<BN == 128, float, double>;
+  constexpr int FLUSH = stats_flush_bytes<BN, WX_THREADS, Acc>();
+  constexpr int LOW = SMEM_EPI > FLUSH ? SMEM_EPI : FLUSH;  // the epilogue tile / statistics scratch
+  constexpr int OFF_RAW = (OFF_B + 2 * BBUF > LOW ? OFF_B + 2 * BBUF : LOW);  // raw halo above both
   constexpr int OFF_SS = OFF_RAW + WX_RAW;
   constexpr int SMEM = OFF_SS + 2 * WX_CK * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
@@ -230,13 +236,7 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
     vrow0[a] = py * 8 + px2;
     vsw0[a] = wx_vswz(py, px2);
   }
-  f32x16 acc[2][MT][2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int a = 0; a < MT; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[p][a][b] = f32x16{};
+  f32x16 acc[2][MT][2];  // (zeroed at each tile's first chunk)
 
   auto mma_step = [&](int vb, int bb, int t) __attribute__((always_inline)) {
     const int dy = t >> 1, sp = t & 1;
@@ -297,8 +297,6 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   float creg = coef_load(njobs > 1 ? 1 : 0);
   __syncthreads();
 
-  using Acc = float;  // (fp32 statistics registers, as the direct kernel at BN = 128)
-  static_assert(stats_flush_bytes<BN, WX_THREADS, Acc>() <= SMEM_EPI, "statistics scratch exceeds the tile");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float amx = 0.0f;
   const TileStats ts = tile_stats(ep, prow, n0, N);
@@ -308,6 +306,12 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
     int img, y0, x0;
     tile_xy(i, img, y0, x0);
     BRegs rb_hold;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[p][a][b] = f32x16{};
     for (int c = 0; c < nchunks; ++c, ++J) {
       const bool has_next = J + 1 < njobs;
       const bool defer = c + 1 == nchunks && has_next;  // next job = next tile: V / weights after the epilogue
@@ -362,12 +366,6 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
       }
       __syncthreads();
     }
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int a = 0; a < MT; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[p][a][b] = f32x16{};
     auto dst = [&](int pix, int cl) -> float* {
       const int y = y0 + pix / WX_TW, x = x0 + pix % WX_TW;
       if (y >= g.h || x >= g.w) return nullptr;
@@ -394,17 +392,19 @@ int64_t conv3x3_persist_rows(const GatherArg& g, int N);
 
 bool conv3x3_wx2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols) {
   return option(SELUNET_OPT_WX2, 1) != 0 && h >= WX_TH && w >= WX_TW && w % 2 == 0 && c_in % WX_CK == 0 &&
-         c_src0 % WX_CK == 0 && c_in >= 64 && c_in <= 512 && n_cols % 128 == 0;
+         c_src0 % WX_CK == 0 && c_in >= 64 && c_in <= 512 && n_cols % 64 == 0;
 }
 
 int conv3x3_wx2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                        const float* amax1, hipStream_t st) {
   const int tiles_x = (int)cdiv(g.w, WX_TW), tiles_y = (int)cdiv(g.h, WX_TH);
-  const int n_tiles = N / 128;
+  const bool bn128 = conv3x3_x2_bn128(N, ep);
+  const int n_tiles = N / (bn128 ? 128 : 64);
   const int gp = (int)conv3x3_persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
   const int ptiles = (int)((int64_t)g.n * tiles_x * tiles_y);
   const int64_t kw = (int64_t)12 * g.Ctot;       // 32-bit words per packed row
-  hipLaunchKernelGGL((conv3x3_wx2_kernel<128>), dim3((unsigned)(gp * n_tiles)), dim3(WX_THREADS), 0, st, g,
+  auto kern = bn128 ? conv3x3_wx2_kernel<128> : conv3x3_wx2_kernel<64>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(gp * n_tiles)), dim3(WX_THREADS), 0, st, g,
                      reinterpret_cast<const unsigned char*>(w), N, ep, n_tiles, tiles_x, tiles_y, ptiles, gp,
                      w + (int64_t)N * kw, amax0, amax1);
   return check_launch("conv3x3_wx2");

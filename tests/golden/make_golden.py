@@ -423,17 +423,23 @@ def kats():
     print(f"wrote {path}: bce={bce:.4f} ce={ce:.4f} miou={data['miou']:.6f} thr={train_thr!r},{eval_thr!r}")
 
 
-def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0, member=0):
+def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0, member=0,
+                 hard=None):
     """mIoU parity run (BASELINE.json 'mIoU parity'): the reference training loop
     (train.py:183-241: forward, BCEWithLogits aux + calc_selective_risk_image_b, Adam, the
     per-batch Evaluator on the fp64-sigmoid masks) for `epochs` passes over a seeded synthetic
     train set in fixed order (no shuffle, no flips), then an eval-mode pass over a validation set
     (train.py:274-318). Records per-step losses, the training-phase confusion matrix, and the
     validation confusion matrices / mIoU (selective and plain Evaluator)."""
-    from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess
+    from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, make_patches_hard, preprocess
 
-    ti, tl = make_patches(n_train, size, seed=2024)
-    vi, vl = make_patches(n_val, size, seed=2025)
+    if hard:  # (contrast, noise, texture, decoys): synthetic.make_patches_hard
+        c, nz, tx, dc = hard
+        gen = lambda n, sd: make_patches_hard(n, size, seed=sd, contrast=c, noise=nz, texture=tx, decoys=int(dc))  # noqa
+    else:
+        gen = lambda n, sd: make_patches(n, size, seed=sd)  # noqa: E731
+    ti, tl = gen(n_train, 2024)
+    vi, vl = gen(n_val, 2025)
     xtr, ltr = preprocess(ti, tl)
     xva, lva = preprocess(vi, vl)
     if member:  # ensemble member: the training inputs perturbed at the rounding level (_perturbed)
@@ -462,7 +468,8 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
             total += lab.numel()
             reject += lab.numel() - int(sel.sum())
             ev.add_batch(lab.numpy().astype("uint8"), pred, selection=sel)
-    out = {"meta_n_train": n_train, "meta_n_val": n_val, "meta_size": size, "meta_bs": bs, "meta_epochs": epochs,
+    out = {"meta_hard": np.array(hard if hard else [], np.float64),
+           "meta_n_train": n_train, "meta_n_val": n_val, "meta_size": size, "meta_bs": bs, "meta_epochs": epochs,
            "meta_lamb": lamb, "meta_seed": seed, "meta_train_seed": 2024, "meta_val_seed": 2025,
            "train_losses": np.array(losses), "train_cm": ev.confusion_matrix.copy(),
            "train_selected": np.int64(total - reject), "train_total": np.int64(total)}
@@ -579,6 +586,11 @@ def _sampled(d, name, g):
 
 
 MIOU256 = dict(fname="miou_sel_256.npz", n_train=128, n_val=256, size=256, bs=16, epochs=16, lamb=2)
+# the discriminative mIoU run: synthetic.make_patches_hard (low contrast, noise, shared stain texture,
+# unlabelled tumor-coloured decoys), so the reference lands well below 1 (MIOU_HARD)
+MIOU_HARD = (0.35, 28.0, 20.0, 6)
+MIOU256H = dict(fname="miou_sel_256h.npz", n_train=128, n_val=256, size=256, bs=16, epochs=16, lamb=2,
+                hard=MIOU_HARD)
 
 
 def miou_spread(k_members=8, fname="miou_sel_64.npz", **kw):
@@ -967,6 +979,19 @@ if __name__ == "__main__":
         np.savez(os.path.join(HERE, f"_miou256_member{k}.npz"), **r)
         print(f"member {k}: val mIoU {float(r['val_miou']):.5f} selective {float(r['val_miou_selective']):.5f} "
               f"train {_miou_cm(r['train_cm']):.5f}", flush=True)
+        sys.exit(0)
+    if sys.argv[1:] == ["miou256h"]:
+        miou_fixture(**MIOU256H)
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256h_member"]:  # one perturbed member of the hard run (run several in parallel)
+        k = int(sys.argv[2])
+        r = miou_fixture(member=k, **MIOU256H)
+        np.savez(os.path.join(HERE, f"_miou256_member{k}.npz"), **r)
+        print(f"member {k}: val mIoU {float(r['val_miou']):.5f} selective {float(r['val_miou_selective']):.5f} "
+              f"train {_miou_cm(r['train_cm']):.5f}", flush=True)
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256h_collect"]:
+        miou_collect(int(sys.argv[2]) if len(sys.argv) > 2 else 8, MIOU256H["fname"])
         sys.exit(0)
     if sys.argv[1:2] == ["miou256_collect"]:
         miou_collect(int(sys.argv[2]) if len(sys.argv) > 2 else 8, MIOU256["fname"])

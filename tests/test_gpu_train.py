@@ -19,7 +19,7 @@ import selectivenet_for_semantic_segmentation_binary_amd as S
 from oracle import unet_b_cpu as O
 from selectivenet_for_semantic_segmentation_binary_amd import data as D
 from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics, logit_threshold, mean_iou
-from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, preprocess
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_patches, make_patches_hard, preprocess
 from tests import _golden as G
 from tests.test_gpu_model import build
 
@@ -95,20 +95,40 @@ def _loop(net, xs, ls, bs, epochs, lamb, training, metrics):
     return np.array(losses)
 
 
+def _miou_data(d):
+    """The fixture's training / validation patches (make_patches, or make_patches_hard with the
+    recorded settings)."""
+    size = int(d["meta_size"])
+    hard = d["meta_hard"] if "meta_hard" in d.files else np.zeros(0)
+    if hard.size:
+        c, nz, tx, dc = (float(v) for v in hard)
+        gen = lambda n, sd: make_patches_hard(n, size, seed=sd, contrast=c, noise=nz, texture=tx,  # noqa: E731
+                                              decoys=int(dc))
+    else:
+        gen = lambda n, sd: make_patches(n, size, seed=sd)  # noqa: E731
+    return (preprocess(*gen(int(d["meta_n_train"]), int(d["meta_train_seed"]))),
+            preprocess(*gen(int(d["meta_n_val"]), int(d["meta_val_seed"]))))
+
+
+MIOU_FIXTURES = [f for f in ("miou_sel_256h.npz", "miou_sel_256.npz") if os.path.exists(os.path.join(G.GOLDEN, f))]
+
+
+@pytest.mark.parametrize("fname", MIOU_FIXTURES)
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 0.002), (torch.bfloat16, 0.01)])
-def test_miou_parity_vs_reference_training(dtype, tol):
+def test_miou_parity_vs_reference_training(dtype, tol, fname):
     """BASELINE.json 'mIoU parity': the reference's training loop (train.py:183-241) run by
-    tests/golden/make_golden.py (miou256) — 16 epochs over 128 seeded synthetic 256x256 patches at
-    batch 16, s_lamb=2, Adam lr 1e-3 — then eval-mode mIoU (Evaluator.get_mIoU,
-    utils/compute_metric.py:60-65; prediction rule of train.py:150) over 256 validation patches; the
-    same run through the HIP path must land within `tol` of the reference's training-phase and
-    validation mIoU. The fixture records the reference's own spread (4 runs on training inputs
-    perturbed by 1e-7 relative, `val_miou_ens`: validation mIoU 0.99876-0.99929 against 0.99944,
-    spread 0.00068), below 0.002 at this size, so `tol` is enforced as is."""
-    d = G.load("miou_sel_256.npz")
-    size, bs, ep, lamb = int(d["meta_size"]), int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
-    xtr, ltr = preprocess(*make_patches(int(d["meta_n_train"]), size, seed=int(d["meta_train_seed"])))
-    xva, lva = preprocess(*make_patches(int(d["meta_n_val"]), size, seed=int(d["meta_val_seed"])))
+    tests/golden/make_golden.py — 16 epochs over 128 seeded synthetic 256x256 patches at batch 16,
+    s_lamb=2, Adam lr 1e-3 — then eval-mode mIoU (Evaluator.get_mIoU, utils/compute_metric.py:60-65;
+    prediction rule of train.py:150) over 256 validation patches; the same run through the HIP path
+    must land within `tol` of the reference's training-phase and validation mIoU. Two data sets:
+    miou_sel_256h.npz (make_golden.py miou256h: synthetic.make_patches_hard — low colour contrast,
+    noise, a stain texture shared by both classes and unlabelled tumor-coloured decoys, so the
+    reference's own validation mIoU is far from 1 and a defect moves it) and miou_sel_256.npz (the
+    easy set: 0.9994). Each fixture records the reference's own spread (runs on training inputs
+    perturbed by 1e-7 relative, `val_miou_ens`), which must sit inside `tol`."""
+    d = G.load(fname)
+    bs, ep, lamb = int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
+    (xtr, ltr), (xva, lva) = _miou_data(d)
     net = build(True, int(d["meta_seed"]), dtype)
     tr = SegMetrics(DEV, selective=True, rule="train")
     losses = _loop(net, torch.tensor(xtr, device=DEV), torch.tensor(ltr, device=DEV), bs, ep, lamb, True, [tr])
@@ -124,7 +144,7 @@ def test_miou_parity_vs_reference_training(dtype, tol):
     m_sel, m_all = mean_iou(vs.confusion_matrix()), mean_iou(vp.confusion_matrix())
     spread = {k: float(np.abs(d[k + "_ens"] - float(d[k])).max()) for k in ("val_miou", "val_miou_selective")
               if k + "_ens" in d.files}
-    line = (f"mIoU [{dtype}]: train {m_tr:.5f} (reference {m_tr_ref:.5f}), val {m_all:.5f} (reference "
+    line = (f"mIoU {fname} [{dtype}]: train {m_tr:.5f} (reference {m_tr_ref:.5f}), val {m_all:.5f} (reference "
             f"{float(d['val_miou']):.5f}), val selective {m_sel:.5f} (reference {float(d['val_miou_selective']):.5f}); "
             f"reference spread {spread}; tol {tol}")
     print(line)

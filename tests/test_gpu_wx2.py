@@ -67,7 +67,8 @@ def test_wx2_pack():
 def test_wx2_eligibility():
     ok = lambda *a: K.query("selunet_conv3x3_wx2_ok", *a)  # noqa: E731
     assert ok(32, 32, 64, 64, 128) == 1
-    assert ok(32, 32, 64, 64, 64) == 0     # 128-column tiles only
+    assert ok(32, 32, 64, 64, 64) == 1     # 64-column tiles
+    assert ok(32, 32, 64, 64, 96) == 0
     assert ok(32, 32, 32, 32, 128) == 0    # one direct-kernel chunk
     assert ok(8, 8, 64, 64, 128) == 0      # below the 16x16 tile
     assert ok(32, 31, 64, 64, 128) == 0    # output pairs need an even width
@@ -81,6 +82,8 @@ def test_wx2_eligibility():
     (256, 0, 128, 2, 32, 32, False),
     (128, 128, 256, 1, 32, 16, True),   # two sources, two column tiles
     (64, 0, 128, 1, 18, 34, True),      # partial tiles in both directions
+    (64, 0, 64, 2, 32, 32, True),       # BN = 64
+    (64, 64, 64, 1, 20, 48, True),      # BN = 64, two sources, partial tiles
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_wx2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
@@ -125,7 +128,8 @@ def test_wx2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
 
 @pytest.mark.parametrize("cin,cout,split,h,w", [(128, 64, 0, 32, 32), (128, 128, 64, 32, 32),
                                                 (256, 128, 128, 16, 48), (128, 256, 0, 20, 24),
-                                                (512, 256, 256, 16, 16), (256, 512, 0, 32, 32)])
+                                                (512, 256, 256, 16, 16), (256, 512, 0, 32, 32),
+                                                (64, 64, 0, 32, 32), (64, 128, 0, 24, 16)])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_wx2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range. The data
