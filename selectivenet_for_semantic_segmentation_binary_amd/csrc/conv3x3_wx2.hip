@@ -26,7 +26,7 @@
 //   t = 2: the raw fp32 halo of job J + 1 (loaded into registers at the previous job's t = 3),
 //          BN+ReLU applied, zero outside the image -> the raw LDS tile;
 //   t = 3: the raw halo and coefficients of job J + 2 -> registers;
-//   t = 4: raw tile -> the four split V planes of job J + 1 (the other V buffer).
+//   t = 4, 5: raw tile -> the four split V planes of job J + 1 (the other V buffer).
 // The weights of step S + 1 are loaded during step S and stored to the other weight buffer after its
 // MFMAs. At a tile's last chunk the V planes and weights of the next tile wait for the LDS-staged
 // epilogue (which spans the V and weight buffers; the raw tile and coefficients sit above it).
@@ -128,20 +128,26 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   struct BRegs {
     uint4 v[B_ROUNDS];
   };
+  // (staging address math is recomputed from an opaque copy of tid at every use: hoisted out of the
+  // chunk loop it stays live through the MFMA steps and spills)
   auto b_load = [&](int st) __attribute__((always_inline)) {  // st: step within a tile (chunk * 6 + t)
     BRegs rb;
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
 #pragma unroll
     for (int r = 0; r < B_ROUNDS; ++r) {
-      const int idx = r * WX_THREADS + tid;
+      const int idx = r * WX_THREADS + tq;
       const int col = idx >> 3, u8 = idx & 7;
       rb.v[r] = *reinterpret_cast<const uint4*>(W + (int64_t)(n0 + col) * wrow + (int64_t)st * 128 + u8 * 16);
     }
     return rb;
   };
   auto b_store = [&](const BRegs& rb, int buf) __attribute__((always_inline)) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
 #pragma unroll
     for (int r = 0; r < B_ROUNDS; ++r) {
-      const int idx = r * WX_THREADS + tid;
+      const int idx = r * WX_THREADS + tq;
       const int col = idx >> 3, u8 = idx & 7;
       const int pl = u8 >> 2, u = u8 & 3;
       *reinterpret_cast<uint4*>(Bs + buf * BBUF + ((pl * BN + col) * 4 + (u ^ wx_bswz(col))) * 16) = rb.v[r];
@@ -159,13 +165,15 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
     int img, y0, x0, c;
     tile_xy(job / nchunks, img, y0, x0);
     const SrcArg sa = chunk_src(job % nchunks, c);
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
 #pragma unroll
     for (int r = 0; r < WX_RAW_ROUNDS; ++r) {
-      const int hp = min((r * WX_THREADS + tid) >> 2, WX_HPIX - 1);
+      const int hp = min((r * WX_THREADS + tq) >> 2, WX_HPIX - 1);
       const int hy = hp / WX_HW, hx = hp - hy * WX_HW;
       const int ys = min(max(y0 - 1 + hy, 0), g.h - 1), xq = min(max(x0 - 1 + hx, 0), g.w - 1);
       rr.v[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(sa.data) +
-                                                (((int64_t)img * g.h + ys) * g.w + xq) * sa.C + c + rcc * 4);
+                                                (((int64_t)img * g.h + ys) * g.w + xq) * sa.C + c + (tq & 3) * 4);
     }
     return rr;
   };
@@ -175,9 +183,11 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
       __attribute__((always_inline)) {
     int img, y0, x0;
     tile_xy(job / nchunks, img, y0, x0);
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
 #pragma unroll
     for (int r = 0; r < WX_RAW_ROUNDS; ++r) {
-      const int hidx = r * WX_THREADS + tid;
+      const int hidx = r * WX_THREADS + tq;
       if (hidx >= WX_HPIX * 4) continue;
       const int hp = hidx >> 2;
       const int hy = hp / WX_HW, hx = hp - hy * WX_HW;
@@ -192,12 +202,14 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
           }
         }
       }
-      *reinterpret_cast<f32x4*>(Raw + hp * 64 + rcc * 16) = v;
+      *reinterpret_cast<f32x4*>(Raw + hp * 64 + (tq & 3) * 16) = v;
     }
   };
-  // raw LDS tile -> the four split V planes of V buffer vb (x2 scale xs)
-  auto form_v = [&](int vb) __attribute__((always_inline)) {
-    for (int s = tid; s < WX_SLOTS; s += WX_THREADS) {
+  // raw LDS tile -> the four split V planes of V buffer vb (x2 scale xs): slots [s0, s1) of the 576
+  auto form_v = [&](int vb, int s0, int s1) __attribute__((always_inline)) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    for (int s = s0 + tq; s < s1; s += WX_THREADS) {
       const int cg = s & 3, px2 = (s >> 2) & 7, hy = s >> 5;
       const unsigned char* rp = Raw + (hy * WX_HW + 2 * px2) * 64 + cg * 16;
       const f32x4 d0 = *reinterpret_cast<const f32x4*>(rp);
@@ -292,7 +304,7 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   }
   b_store(b_load(0), 0);
   __syncthreads();
-  if (njobs > 0) form_v(0);
+  if (njobs > 0) form_v(0, 0, WX_SLOTS);
   RawRegs ra = raw_load(njobs > 1 ? 1 : 0);
   float creg = coef_load(njobs > 1 ? 1 : 0);
   __syncthreads();
@@ -328,7 +340,9 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
           ra = raw_load(J + 2);
           creg = coef_load(J + 2);
         }
-        if (t == 4 && has_next && !defer) form_v((J + 1) & 1);
+        // (slots 0-511 at t = 4, the last 64 — wave 0 — at t = 5)
+        if (t == 4 && has_next && !defer) form_v((J + 1) & 1, 0, WX_THREADS);
+        if (t == 5 && has_next && !defer) form_v((J + 1) & 1, WX_THREADS, WX_SLOTS);
         if (defer && t == STEPS - 1) rb_hold = rb;
         else b_store(rb, (S + 1) & 1);
         __syncthreads();
@@ -380,7 +394,7 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
     lds_tile_store_acc<float, WX_TH * WX_TW, BN, WX_THREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
     if (i + 1 < ntl) {
       __syncthreads();  // the tile has been read: LDS back to V planes / weights
-      form_v(J & 1);    // (J is the next tile's first job; its raw halo was staged at t = 2)
+      form_v(J & 1, 0, WX_SLOTS);  // (J is the next tile's first job; its raw halo was staged at t = 2)
       b_store(rb_hold, S & 1);
       __syncthreads();
     }
