@@ -27,7 +27,7 @@ LAYERS = [
 ]
 
 
-def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False, x2=False):
+def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False, x2=False, wx2=False):
     dev = "cuda"
     srcs = []
     keep = []
@@ -77,7 +77,17 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
         keep.append(amax)
         name = K.query("selunet_conv3x3_x2_kernel_name", co, ep.mode, ep.split).decode()
 
+    if wx2:  # split-fp16 Winograd F(2,3): [co][12*ci] words + co unscale factors (random: timing only)
+        w = torch.randn(co * 12 * ci + co, device=dev).abs() * 1e-3 + 1e-3
+        amax = torch.full((1,), 8.0, device=dev)
+        keep.append(amax)
+        name = "conv3x3_wx2<f32,%d>" % (128 if co % 128 == 0 else 64)
+
     def call():
+        if wx2:
+            K.call("selunet_conv3x3_wx2", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.ptr(amax), K.ptr(amax),
+                   K.stream_ptr())
+            return
         if x2:
             K.call("selunet_conv3x3_x2", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.ptr(amax), K.ptr(amax),
                    K.stream_ptr())
@@ -164,6 +174,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--wino", action="store_true", help="fp32 Winograd F(2,3) kernel (direct-conv FLOPs reported)")
     ap.add_argument("--x2", action="store_true", help="fp32 on split-fp16 operands (selunet_conv3x3_x2)")
+    ap.add_argument("--wx2", action="store_true", help="fp32 split-fp16 Winograd F(2,3) (selunet_conv3x3_wx2)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     sel = set(a.layers.split(",")) if a.layers else None
@@ -172,7 +183,7 @@ def main():
         if sel and name not in sel:
             continue
         if a.only not in ("dgrad", "wgrad"):
-            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino, a.x2)
+            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino, a.x2, a.wx2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
@@ -183,7 +194,7 @@ def main():
             print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
             continue
         if a.only != "fwd":
-            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino, a.x2)
+            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino, a.x2, a.wx2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"dgrad {name:8s} {co:4d}->{c0 + c1:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
