@@ -41,6 +41,10 @@ def run(xtr, ltr, xva, lva, a, member):
         if a.lr_decay and ep == a.epochs // 2:
             for g in opt.param_groups:
                 g["lr"] = a.lr * a.lr_decay
+        if a.cosine:  # train.py:100-101,246-250: CosineAnnealingLR(T_max=epochs, eta_min=lr_min), per epoch
+            lr = a.lr_min + (a.lr - a.lr_min) * (1 + np.cos(np.pi * ep / a.epochs)) / 2
+            for g in opt.param_groups:
+                g["lr"] = lr
         for b0 in range(0, xt.shape[0], a.bs):
             x, lab = xt[b0:b0 + a.bs], lt[b0:b0 + a.bs]
             o, s, ax = net(x)
@@ -69,6 +73,8 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--lr-decay", type=float, default=0.0, help="multiply lr by this at half the epochs")
     ap.add_argument("--lamb", type=float, default=2)
+    ap.add_argument("--cosine", action="store_true", help="cosine-annealed lr per epoch down to --lr-min")
+    ap.add_argument("--lr-min", type=float, default=1e-5)
     ap.add_argument("-k", type=int, default=8)
     ap.add_argument("--hard", default="", help="';'-separated make_patches_hard settings "
                     "'contrast,noise,texture,decoys' to sweep (empty: make_patches)")
