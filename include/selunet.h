@@ -54,7 +54,8 @@ enum {
   SELUNET_OPT_RF_SINGLE,          /* slab rows reduced in one launch by the fused reductions (1024) */
   SELUNET_OPT_APPLY_U8,           /* BN-backward apply: 8 channel groups per thread (0) */
   SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
-  SELUNET_OPT_WX2,                /* split-fp16 3x3 layers on the Winograd F(2,3) kernel where eligible (1) */
+  SELUNET_OPT_WX2,                /* selunet_conv3x3_wx2_ok admits layers to the split-fp16 Winograd kernel (0:
+                                   * measured slower than selunet_conv3x3_x2 on every UNet_B layer) */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
@@ -218,8 +219,9 @@ const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t
  * row (fp64, rounded once, then split); y(x) = (M0 + M1) + M2, y(x+1) = (M1 - M2) - M3. Four fp16
  * products per output pair and kernel row instead of six: 2/3 of selunet_conv3x3_x2's MFMAs. w: a
  * SELUNET_PACK_CONV3X3_WX2 pack. Same gathers, range words, epilogues and statistics slab rows as
- * selunet_conv3x3_x2; selunet_conv3x3_wx2_ok tells whether a layer can take it (h, w >= 16, w even,
- * C and c_src0 multiples of 16, C >= 64, n_cols a multiple of 64). */
+ * selunet_conv3x3_x2; selunet_conv3x3_wx2_ok tells whether a layer should take it (SELUNET_OPT_WX2 set, and
+ * h, w >= 16, w even, C and c_src0 multiples of 16, 64 <= C <= 512, n_cols a multiple of 64). At bs=128 it
+ * measured 5-35 % slower than selunet_conv3x3_x2 per layer, so the option is off by default. */
 int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
 int selunet_conv3x3_wx2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                         const float* amax0, const float* amax1, void* stream);

@@ -409,7 +409,7 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
 int64_t conv3x3_persist_rows(const GatherArg& g, int N);
 
 bool conv3x3_wx2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols) {
-  return option(SELUNET_OPT_WX2, 1) != 0 && h >= WX_TH && w >= WX_TW && w % 2 == 0 && c_in % WX_CK == 0 &&
+  return h >= WX_TH && w >= WX_TW && w % 2 == 0 && c_in % WX_CK == 0 &&
          c_src0 % WX_CK == 0 && c_in >= 64 && c_in <= 512 && n_cols % 64 == 0;
 }
 

@@ -1194,7 +1194,8 @@ extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32
 }
 
 extern "C" int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols) {
-  return halo_enabled() && conv3x3_x2_shape_ok(h, w, c_in, c_src0, n_cols) &&
+  // (measured slower than selunet_conv3x3_x2 on every UNet_B layer: off unless SELUNET_OPT_WX2 = 1)
+  return option(SELUNET_OPT_WX2, 0) != 0 && halo_enabled() && conv3x3_x2_shape_ok(h, w, c_in, c_src0, n_cols) &&
                  conv3x3_wx2_shape_ok(h, w, c_in, c_src0, n_cols)
              ? 1
              : 0;

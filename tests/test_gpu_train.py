@@ -76,11 +76,17 @@ def test_seg_metrics_bit_exact(rule):
         assert selected == (2 * int(smask.sum()) if selective else 2 * p)
 
 
-def _loop(net, xs, ls, bs, epochs, lamb, training, metrics):
+def _loop(net, xs, ls, bs, epochs, lamb, training, metrics, cosine_min=0.0):
     loss_A = S.BCEWithLogitsLoss()
     opt = S.Adam(net.parameters(), lr=1e-3) if training else None
+    # the reference's CosineAnnealingLR(T_max=epochs, eta_min=cosine_min), stepped once per epoch
+    # (train.py:100-101, 246-250), as a plain torch scheduler on the package's torch-compatible Adam
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=epochs, eta_min=cosine_min) \
+        if training and cosine_min > 0 else None
     losses = []
-    for _ in range(epochs):
+    for ep in range(epochs):
+        if sched is not None and ep > 0:
+            sched.step()
         for b0 in range(0, xs.shape[0], bs):
             x, lab = xs[b0:b0 + bs], ls[b0:b0 + bs]
             o, s, a = net(x)
@@ -131,7 +137,8 @@ def test_miou_parity_vs_reference_training(dtype, tol, fname):
     (xtr, ltr), (xva, lva) = _miou_data(d)
     net = build(True, int(d["meta_seed"]), dtype)
     tr = SegMetrics(DEV, selective=True, rule="train")
-    losses = _loop(net, torch.tensor(xtr, device=DEV), torch.tensor(ltr, device=DEV), bs, ep, lamb, True, [tr])
+    cmin = float(d["meta_cosine_min"]) if "meta_cosine_min" in d.files else 0.0
+    losses = _loop(net, torch.tensor(xtr, device=DEV), torch.tensor(ltr, device=DEV), bs, ep, lamb, True, [tr], cmin)
     ref_losses = d["train_losses"]
     print(f"train loss {losses[0]:.5f}->{losses[-1]:.5f} (reference {ref_losses[0]:.5f}->{ref_losses[-1]:.5f})")
     assert abs(losses[0] - ref_losses[0]) < (1e-4 if dtype == torch.float32 else 2e-2) * abs(ref_losses[0])

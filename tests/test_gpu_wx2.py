@@ -22,6 +22,15 @@ DEV = "cuda"
 TOL = 2e-6
 
 
+@pytest.fixture(autouse=True)
+def wx2_on():
+    """selunet_conv3x3_wx2_ok admits layers only with SELUNET_OPT_WX2 set (off by default: measured slower
+    than the direct split-fp16 kernel); the kernel itself is tested here either way."""
+    prev = K.set_option("WX2", 1)
+    yield
+    K.set_option("WX2", prev)
+
+
 def pack_wx2(w, dgrad=True):
     co, ci = w.shape[:2]
     wd = w.to(DEV).contiguous()
