@@ -212,6 +212,10 @@ int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, f
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
+/* Statistics slab rows (stats / colsum / BN-backward sums of the epilogue) selunet_conv3x3_x2 and
+ * selunet_conv3x3_wx2 write for this operand: n_cols == 64 runs the 64-column kernel with two
+ * 256-thread workgroups per CU (min(16x16 tiles, 512) rows), others as selunet_gemm_stats_rows. */
+int64_t selunet_conv3x3_x2_stats_rows(const selunet_gather* a, int32_t n_cols);
 /* The same fp32 3x3 conv forward / data gradient on split-fp16 operands as a 1-D Winograd F(2,3) along
  * x (model.py:11): per kernel row dy and output pair (x, x+1), M_xi = sum_c U_xi[c] * V_xi[c] over
  * V = (d0 - d2, d1 + d2, d2 - d1, d1 - d3) of the four inputs x-1..x+2 (formed in fp32 from the

@@ -95,6 +95,7 @@ SIGNATURES = {
     "selunet_conv3x3_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
     "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
     "selunet_conv3x3_wx2_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "selunet_conv3x3_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
     "selunet_conv3x3_wx2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
     "selunet_act_bound": (c_int32, [P, P, c_int32, c_int64, P, P]),
     "selunet_conv3x3_wgrad_x2_ws_bytes": (c_int64, [ctypes.POINTER(Gather), ctypes.POINTER(Gather)]),

@@ -2116,6 +2116,7 @@ static int persist_rows(const GatherArg& g, int N) {
 }
 
 int64_t conv3x3_persist_rows(const GatherArg& g, int N) { return persist_rows(g, N); }
+int conv3x3_persist_wgs() { return PERSIST_WGS; }
 
 bool conv3x3_halo_persistent(const GatherArg& g, int dtype) { return !halo_one_chunk(g, dtype) && persist_enabled(); }
 
@@ -2207,6 +2208,7 @@ bool conv3x3_x2_bn128(int N, const EpiArg& ep) {
 
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st) {
+  if (conv3x3_x2d_eligible(g, N)) return conv3x3_x2d_launch(g, w, ep, amax0, amax1, st);  // 64 columns
   if (conv3x3_x2_bn128(N, ep)) launch_x2<128>(g, w, N, ep, amax0, amax1, st);
   else launch_x2<64>(g, w, N, ep, amax0, amax1, st);
   return check_launch("conv3x3_x2");

@@ -418,7 +418,8 @@ int conv3x3_wx2_launch(const GatherArg& g, const float* w, int N, const EpiArg& 
   const int tiles_x = (int)cdiv(g.w, WX_TW), tiles_y = (int)cdiv(g.h, WX_TH);
   const bool bn128 = conv3x3_x2_bn128(N, ep);
   const int n_tiles = N / (bn128 ? 128 : 64);
-  const int gp = (int)conv3x3_persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
+  // = the statistics slab rows of selunet_conv3x3_x2_stats_rows
+  const int gp = (int)(conv3x3_x2d_eligible(g, N) ? conv3x3_x2d_rows(g) : conv3x3_persist_rows(g, N));
   const int ptiles = (int)((int64_t)g.n * tiles_x * tiles_y);
   const int64_t kw = (int64_t)12 * g.Ctot;       // 32-bit words per packed row
   auto kern = bn128 ? conv3x3_wx2_kernel<128> : conv3x3_wx2_kernel<64>;

@@ -1173,7 +1173,15 @@ extern "C" const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mo
   EpiArg e{};
   e.mode = mode;
   e.split = split;
+  if (n_cols == 64) return "conv3x3_x2d<f32,64>";
   return conv3x3_x2_bn128(n_cols, e) ? "conv3x3_x2<f32,128>" : "conv3x3_x2<f32,64>";
+}
+
+extern "C" int64_t selunet_conv3x3_x2_stats_rows(const selunet_gather* a, int32_t n_cols) {
+  GatherArg g;
+  if (make_gather(a, SELUNET_F32, g, 4)) return -1;
+  if (conv3x3_x2d_eligible(g, n_cols)) return conv3x3_x2d_rows(g);
+  return conv3x3_halo_stats_rows(g, n_cols, SELUNET_F32);
 }
 
 extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,

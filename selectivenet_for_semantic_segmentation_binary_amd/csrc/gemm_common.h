@@ -471,6 +471,12 @@ bool conv3x3_wx2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
 int conv3x3_wx2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                        const float* amax1, hipStream_t st);
 int64_t conv3x3_persist_rows(const GatherArg& g, int N);  // workgroup rows of the persistent 3x3 kernels
+int conv3x3_persist_wgs();  // their workgroup target (selunet_set_halo_workgroups; default 256 = one per CU)
+// the 64-column split-fp16 kernel, two 256-thread workgroups per CU (conv3x3_x2d.hip)
+bool conv3x3_x2d_eligible(const GatherArg& g, int N);
+int64_t conv3x3_x2d_rows(const GatherArg& g);
+int conv3x3_x2d_launch(const GatherArg& g, const float* w, const EpiArg& ep, const float* amax0, const float* amax1,
+                       hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,

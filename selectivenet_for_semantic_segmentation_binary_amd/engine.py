@@ -334,7 +334,8 @@ class Engine:
             rows = K.query("selunet_first_conv_rows", n, h, w)
         else:
             g = K.gather(n, h, w, taps, *srcs)
-            rows = K.query("selunet_gemm_stats_rows", g, co, self.code)
+            rows = (K.query("selunet_conv3x3_x2_stats_rows", g, co) if wp.mode in X2_MODES
+                    else K.query("selunet_gemm_stats_rows", g, co, self.code))
         center = None
         if ctx.training:
             stats = K.keep(torch.empty(rows, 2, co, dtype=torch.float32, device=dev))
@@ -625,7 +626,8 @@ class Engine:
         wd = wp.dgrad
         dsrc = K.source(dy, co, amax=dyw)
         ga = K.gather(st.n, st.h, st.w, 9, dsrc)
-        rows = K.query("selunet_gemm_stats_rows", ga, ci, self.code)
+        rows = (K.query("selunet_conv3x3_x2_stats_rows", ga, ci) if wp.mode in X2_MODES
+                else K.query("selunet_gemm_stats_rows", ga, ci, self.code))
         if dgrad_split is None:
             dx = K.keep(torch.empty(M, ci, dtype=self.dt, device=dev))
             ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)

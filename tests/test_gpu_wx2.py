@@ -121,7 +121,7 @@ def test_wx2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
     M = n * h * w
     y = torch.empty(M, cout, device=DEV)
     g = K.gather(n, h, w, 9, *srcs)
-    rows = K.query("selunet_gemm_stats_rows", g, cout, K.F32)
+    rows = K.query("selunet_conv3x3_x2_stats_rows", g, cout)
     stats = torch.empty(rows, 2, cout, device=DEV)
     amo = torch.zeros(1, device=DEV)
     ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
@@ -155,7 +155,7 @@ def test_wx2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     dyd = nhwc(dy).to(DEV)  # kept alive: K.source holds the raw pointer
     am = word(dy.abs().max())
     g = K.gather(n, h, w, 9, K.source(dyd, cout))
-    rows = K.query("selunet_gemm_stats_rows", g, cin, K.F32)
+    rows = K.query("selunet_conv3x3_x2_stats_rows", g, cin)
     if split:
         d0 = torch.empty(M, split, device=DEV)
         d1 = torch.empty(M, cin - split, device=DEV)
@@ -183,4 +183,4 @@ def test_wx2_matches_direct_x2_statistics_rows():
     """Same statistics slab rows as the direct split-fp16 kernel (the engine sizes slabs by the query)."""
     x = torch.zeros(2 * 64 * 64, 128, device=DEV)
     g = K.gather(2, 64, 64, 9, K.source(x, 128))
-    assert K.query("selunet_gemm_stats_rows", g, 256, K.F32) > 0
+    assert K.query("selunet_conv3x3_x2_stats_rows", g, 256) == K.query("selunet_gemm_stats_rows", g, 256, K.F32)

@@ -79,6 +79,8 @@ def word(v):
     (256, 0, 128, 2, 32, 32, False),
     (128, 128, 64, 1, 32, 16, True),    # two sources, BN = 64
     (64, 0, 128, 1, 18, 35, True),      # partial tiles in both directions, odd width
+    (64, 0, 64, 2, 64, 48, True),       # 64 columns (two workgroups per CU): several tiles per workgroup
+    (64, 64, 64, 1, 40, 72, True),      # 64 columns, two sources, partial tiles, four chunks
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
@@ -107,7 +109,7 @@ def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
     M = n * h * w
     y = torch.empty(M, cout, device=DEV)
     g = K.gather(n, h, w, 9, *srcs)
-    rows = K.query("selunet_gemm_stats_rows", g, cout, K.F32)
+    rows = K.query("selunet_conv3x3_x2_stats_rows", g, cout)
     stats = torch.empty(rows, 2, cout, device=DEV)
     ep = K.Epilogue(K.ptr(y), None, None, K.ptr(stats), K.EP_PLAIN, 0)
     K.call("selunet_conv3x3_x2", g, K.ptr(u), cout, ep, K.ptr(am0), K.ptr(am1), K.stream_ptr())
@@ -120,7 +122,8 @@ def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
 
 @pytest.mark.parametrize("cin,cout,split,h,w", [(64, 64, 0, 32, 32), (128, 64, 64, 32, 32),
                                                 (256, 128, 128, 16, 48), (128, 256, 0, 20, 24),
-                                                (512, 256, 256, 16, 16)])
+                                                (512, 256, 256, 16, 16), (64, 64, 0, 64, 48),
+                                                (64, 128, 0, 48, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
 def test_x2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range."""
@@ -135,7 +138,7 @@ def test_x2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
     dyd = nhwc(dy).to(DEV)  # kept alive: K.source holds the raw pointer
     am = word(dy.abs().max())
     g = K.gather(n, h, w, 9, K.source(dyd, cout))
-    rows = K.query("selunet_gemm_stats_rows", g, cin, K.F32)
+    rows = K.query("selunet_conv3x3_x2_stats_rows", g, cin)
     if split:
         d0 = torch.empty(M, split, device=DEV)
         d1 = torch.empty(M, cin - split, device=DEV)

@@ -44,7 +44,8 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
     w = (torch.randn(co, kp, device=dev) * 0.05).to(dt)
     g = K.gather(n, hw, hw, 9, *srcs)
     m = n * hw * hw
-    rows = K.query("selunet_gemm_stats_rows", ctypes.byref(g), co, K.dtype_code(dt))
+    rows = (K.query("selunet_conv3x3_x2_stats_rows", ctypes.byref(g), co) if (x2 or wx2)
+            else K.query("selunet_gemm_stats_rows", ctypes.byref(g), co, K.dtype_code(dt)))
     stats = torch.empty(rows, 2, co, device=dev) if not split else None
     if split:  # as in the step: the ConvTranspose2d bias sums of out0 and its range word
         o0 = torch.empty(m, co // 2, device=dev, dtype=dt)
