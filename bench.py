@@ -147,7 +147,7 @@ class KernelTimer:
             return kname, "mfma", flops, nbytes, f"wino {g.h}x{g.w} C={c} N={n_cols} mode={ep.mode}"
         if name == "selunet_conv3x3_x2":  # (g, w, n_cols, ep, amax0, amax1, stream): split-fp16 fp32 conv
             g, n_cols, ep = args[0], _i(args[2]), args[3]
-            kname = K.query("selunet_conv3x3_x2_kernel_name", n_cols, ep.mode, ep.split).decode()
+            kname = K.query("selunet_conv3x3_x2_kernel_name", g, n_cols, ep.mode, ep.split).decode()
             m = g.n * g.h * g.w
             # the fp16 MFMA work executed: three products (hh, hl, lh) per fp32 product, against the
             # fp16 dense peak ("mfma_f16")

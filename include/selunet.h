@@ -56,6 +56,9 @@ enum {
   SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
   SELUNET_OPT_WX2,                /* selunet_conv3x3_wx2_ok admits layers to the split-fp16 Winograd kernel (0:
                                    * measured slower than selunet_conv3x3_x2 on every UNet_B layer) */
+  SELUNET_OPT_X2D,                /* 64-column split-fp16 3x3 layers on the two-workgroups-per-CU kernel: 0 never,
+                                   * 1 every eligible layer, 2 inputs of at most 64 channels, 3 (default) those of
+                                   * them whose source carries a BN+ReLU transform (the forwards) */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
@@ -211,10 +214,11 @@ int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, f
                              void* stream);
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
-const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split);
+const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, int32_t n_cols, int32_t mode, int32_t split);
 /* Statistics slab rows (stats / colsum / BN-backward sums of the epilogue) selunet_conv3x3_x2 and
- * selunet_conv3x3_wx2 write for this operand: n_cols == 64 runs the 64-column kernel with two
- * 256-thread workgroups per CU (min(16x16 tiles, 512) rows), others as selunet_gemm_stats_rows. */
+ * selunet_conv3x3_wx2 write for this operand: the layers SELUNET_OPT_X2D sends to the 64-column kernel
+ * with two 256-thread workgroups per CU have min(16x16 tiles, 512) rows, others as
+ * selunet_gemm_stats_rows. selunet_conv3x3_x2_kernel_name names the kernel a call would run. */
 int64_t selunet_conv3x3_x2_stats_rows(const selunet_gather* a, int32_t n_cols);
 /* The same fp32 3x3 conv forward / data gradient on split-fp16 operands as a 1-D Winograd F(2,3) along
  * x (model.py:11): per kernel row dy and output pair (x, x+1), M_xi = sum_c U_xi[c] * V_xi[c] over

@@ -93,7 +93,7 @@ SIGNATURES = {
     "selunet_gemm_gather_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, c_int32, ctypes.POINTER(Epilogue), P, P,
                                          P]),
     "selunet_conv3x3_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
-    "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [c_int32, c_int32, c_int32]),
+    "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(Gather), c_int32, c_int32, c_int32]),
     "selunet_conv3x3_wx2_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "selunet_conv3x3_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
     "selunet_conv3x3_wx2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
@@ -231,7 +231,7 @@ def load(auto_build: bool = False):
 # selunet_option keys (include/selunet.h)
 OPT = {name: i for i, name in enumerate([
     "HALO", "HALO_PERSIST", "WINO", "WINO_WGRAD", "WINO_WGRAD_TW", "WINO_WGRAD_WAVES", "WGRAD_WGS",
-    "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "WX2"])}
+    "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "WX2", "X2D"])}
 # environment variables the host maps onto options at load (A/B and ablation runs of tools/ and the
 # exact-fp32 comparison paths of the tests); SELUNET_NO_HALO=1 means HALO=0
 ENV_OPTIONS = {f"SELUNET_{k}": v for k, v in OPT.items() if k != "HALO"}

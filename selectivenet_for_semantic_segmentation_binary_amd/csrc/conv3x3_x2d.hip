@@ -327,7 +327,15 @@ int64_t conv3x3_x2d_rows(const GatherArg& g) {
   return std::max<int64_t>(1, std::min<int64_t>(pt, 2 * (int64_t)conv3x3_persist_wgs()));
 }
 
-bool conv3x3_x2d_eligible(const GatherArg& g, int N) { return N == XD_BN && g.Ctot % XD_CK == 0 && g.Ctot <= 1024; }
+// Measured per layer against conv3x3_halo_persist_kernel<float, 64, X2> (tools/conv_bench.py --x2, same box,
+// two runs each): forwards of 64-channel inputs 2-6 % faster, data gradients and the 128-channel inputs
+// 1-4 % slower, hence the default (SELUNET_OPT_X2D 3: 64-channel inputs with a BN+ReLU source = forwards).
+bool conv3x3_x2d_eligible(const GatherArg& g, int N) {
+  const int64_t mode = option(SELUNET_OPT_X2D, 3);
+  if (N != XD_BN || g.Ctot % XD_CK != 0 || mode <= 0) return false;
+  if (mode == 1) return g.Ctot <= 1024;
+  return g.Ctot <= 64 && (mode == 2 || g.src[0].scale != nullptr);
+}
 
 int conv3x3_x2d_launch(const GatherArg& g, const float* w, const EpiArg& ep, const float* amax0, const float* amax1,
                        hipStream_t st) {

@@ -1169,11 +1169,14 @@ extern "C" int32_t selunet_conv3x3_x2_ok(int32_t h, int32_t w, int32_t c_in, int
   return halo_enabled() && conv3x3_x2_shape_ok(h, w, c_in, c_src0, n_cols) ? 1 : 0;
 }
 
-extern "C" const char* selunet_conv3x3_x2_kernel_name(int32_t n_cols, int32_t mode, int32_t split) {
+extern "C" const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, int32_t n_cols, int32_t mode,
+                                                      int32_t split) {
   EpiArg e{};
   e.mode = mode;
   e.split = split;
-  if (n_cols == 64) return "conv3x3_x2d<f32,64>";
+  GatherArg g;
+  if (make_gather(a, SELUNET_F32, g, 4)) return "?";
+  if (conv3x3_x2d_eligible(g, n_cols)) return "conv3x3_x2d<f32,64>";
   return conv3x3_x2_bn128(n_cols, e) ? "conv3x3_x2<f32,128>" : "conv3x3_x2<f32,64>";
 }
 

@@ -87,6 +87,23 @@ def test_host_queries_need_no_device(lib):
     g = K.gather(2, 8, 8, 1, K.source(fake, 64))  # 1x1 taps: generic kernel, one stats row per 128 pixels
     assert K.query("selunet_gemm_stats_rows", ctypes.byref(g), 64, K.BF16) == 1
     assert K.query("selunet_gemm_kernel_name", ctypes.byref(g), None, 64, K.EP_PLAIN, K.BF16) == b"gemm_gather<bf16>"
+    # split-fp16 3x3 conv, 64 columns: the option SELUNET_OPT_X2D picks the kernel and its slab rows
+    f32 = torch.empty(64, dtype=torch.float32)
+    scale = torch.ones(64)
+    fwd = K.gather(4, 64, 64, 9, K.source(f32, 64, scale, scale))  # BN+ReLU source: a forward
+    dgr = K.gather(4, 64, 64, 9, K.source(f32, 64))
+    name = lambda g: K.query("selunet_conv3x3_x2_kernel_name", ctypes.byref(g), 64, K.EP_PLAIN, 0)  # noqa: E731
+    rows = lambda g: K.query("selunet_conv3x3_x2_stats_rows", ctypes.byref(g), 64)  # noqa: E731
+    prev = K.set_option("X2D", -1)
+    try:
+        assert name(fwd) == b"conv3x3_x2d<f32,64>" and rows(fwd) == 4 * 4 * 4  # one row per 16x16 tile
+        assert name(dgr) == b"conv3x3_x2<f32,64>"
+        K.set_option("X2D", 0)
+        assert name(fwd) == b"conv3x3_x2<f32,64>"
+        K.set_option("X2D", 1)
+        assert name(dgr) == b"conv3x3_x2d<f32,64>"
+    finally:
+        K.set_option("X2D", prev)
 
 
 def test_invalid_arguments_fail_with_a_message(lib):

@@ -21,6 +21,18 @@ DEV = "cuda"
 TOL = 2e-6
 
 
+@pytest.fixture
+def x2d():
+    """Set SELUNET_OPT_X2D for one test (1: every 64-column layer on conv3x3_x2d_kernel, 0: none)."""
+    prev = []
+
+    def setter(mode):
+        prev.append(K.set_option("X2D", mode))
+    yield setter
+    for v in prev[:1]:
+        K.set_option("X2D", v)
+
+
 def pack_x2(w, dgrad=True):
     """Split-fp16 operands of a conv3x3 weight [co][ci][3][3] through selunet_pack_weights: fwd
     [co][9*ci] words + co unscale factors, dgrad [ci][9*co] + ci."""
@@ -83,8 +95,10 @@ def word(v):
     (64, 64, 64, 1, 40, 72, True),      # 64 columns, two sources, partial tiles, four chunks
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
-def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
+@pytest.mark.parametrize("x2d_mode", [1, 0])
+def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, halo_wgs, x2d):
     halo_wgs(wgs)
+    x2d(x2d_mode)
     x0 = gen(n, cin0, h, w, seed=1)
     x1 = gen(n, cin1, h, w, seed=2) * 1e-3 if cin1 else None  # sources of different ranges
     wt = gen(cout, cin0 + cin1, 3, 3, seed=3, scale=0.05)
@@ -125,9 +139,11 @@ def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, halo_wgs):
                                                 (512, 256, 256, 16, 16), (64, 64, 0, 64, 48),
                                                 (64, 128, 0, 48, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
-def test_x2_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+@pytest.mark.parametrize("x2d_mode", [1, 0])
+def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, halo_wgs, x2d):
     """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range."""
     halo_wgs(wgs)
+    x2d(x2d_mode)
     n = 2
     wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
     dy = gen(n, cout, h, w, seed=7) * 1e-9

@@ -76,7 +76,7 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
         w = torch.randn(co * kp + co, device=dev).abs() * 1e-3 + 1e-3
         amax = torch.full((1,), 8.0, device=dev)
         keep.append(amax)
-        name = K.query("selunet_conv3x3_x2_kernel_name", co, ep.mode, ep.split).decode()
+        name = K.query("selunet_conv3x3_x2_kernel_name", ctypes.byref(g), co, ep.mode, ep.split).decode()
 
     if wx2:  # split-fp16 Winograd F(2,3): [co][12*ci] words + co unscale factors (random: timing only)
         w = torch.randn(co * 12 * ci + co, device=dev).abs() * 1e-3 + 1e-3
