@@ -32,6 +32,8 @@ NAME_MAP = [
     (r"gemm_wgrad_x2_kernel", "gemm_wgrad_x2<f32>"),
     (_pat("conv3x3_halo_persist_kernel", "f32", 128, "true"), "conv3x3_x2<f32,128>"),
     (_pat("conv3x3_halo_persist_kernel", "f32", 64, "true"), "conv3x3_x2<f32,64>"),
+    (r"conv3x3_x2d_kernel", "conv3x3_x2d<f32,64>"),
+    (r"conv3x3_wx2_kernel", "conv3x3_wx2<f32>"),
     (_pat("conv3x3_wgrad_x2_kernel", 128), "conv3x3_wgrad_x2<128>"),
     (_pat("conv3x3_wgrad_x2_kernel", 64), "conv3x3_wgrad_x2<64>"),
 ]
