@@ -996,6 +996,8 @@ extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_co
   GatherArg g;
   if (make_gather(a, dtype, g, 16 / esz)) return -1;
   if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_stats_rows(g, n_cols, dtype);
+  // the bf16 ConvTranspose2d data gradient (BN-backward sums): the resident-weight kernel's rows
+  if (dtype == SELUNET_BF16 && convt_dgrad_bf16_ntb(g, n_cols) > 0) return convt_dgrad_bf16_rows(g, n_cols);
   return gather_rows(g, n_cols);
 }
 
@@ -1019,6 +1021,8 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
       return bf ? (bn128 ? "conv3x3_halo<bf16,128>" : "conv3x3_halo<bf16,64>")
                 : (bn128 ? "conv3x3_halo<f32,128>" : "conv3x3_halo<f32,64>");
     }
+    if (bf && mode == SELUNET_EP_SCATTER2X && convt_bf16_fwd_ntb(g, n_cols) > 0) return "convt<bf16>";
+    if (bf && mode == SELUNET_EP_PLAIN && convt_dgrad_bf16_ntb(g, n_cols) > 0) return "convt_dgrad<bf16>";
     return bf ? "gemm_gather<bf16>" : "gemm_gather<f32>";
   }
   GatherArg gq;
@@ -1072,6 +1076,14 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
   hipStream_t st = as_stream(stream);
   if (ep->mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype))
     return conv3x3_halo_launch(g, b, n_cols, k_pad, e, dtype, st);
+  if (dtype == SELUNET_BF16) {  // ConvTranspose2d forward / data gradient: the resident-weight kernels
+    if (convt_bf16_eligible(g, n_cols, e) || convt_dgrad_bf16_eligible(g, n_cols, e))
+      return convt_bf16_launch(g, b, n_cols, e, st);
+    SELUNET_REQUIRE(convt_dgrad_bf16_ntb(g, n_cols) == 0 || (e.stats == nullptr && e.colsum == nullptr &&
+                                                             e.bnb.slab == nullptr),
+                    "gemm_gather: statistics epilogue on a ConvTranspose2d data-gradient operand that "
+                    "selunet_gemm_stats_rows sizes for the resident-weight kernel (PLAIN, no amax / bias)");
+  }
   const bool bn128 = n_cols % 128 == 0 && !(ep->mode == SELUNET_EP_SPLIT && ep->split % 128 != 0);
   if (dtype == SELUNET_F32) {
     if (bn128) launch_gather<float, 128>(g, b, n_cols, k_pad, e, st);

@@ -464,6 +464,12 @@ int64_t convt_dgrad_x2_rows(const GatherArg& g, int N);
 bool convt_dgrad_x2_eligible(const GatherArg& g, int N, const EpiArg& e);
 int convt_dgrad_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                           hipStream_t st);
+int convt_bf16_fwd_ntb(const GatherArg& g, int N);  // bf16 resident-weight ConvTranspose2d (convt_bf16.hip)
+int convt_dgrad_bf16_ntb(const GatherArg& g, int N);
+int64_t convt_dgrad_bf16_rows(const GatherArg& g, int N);
+bool convt_bf16_eligible(const GatherArg& g, int N, const EpiArg& e);
+bool convt_dgrad_bf16_eligible(const GatherArg& g, int N, const EpiArg& e);
+int convt_bf16_launch(const GatherArg& g, const void* w, int N, const EpiArg& e, hipStream_t st);
 int convt_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                     hipStream_t st);
 // the same on the split-fp16 1-D Winograd F(2,3) kernel (conv3x3_wx2.hip, selunet_conv3x3_wx2)
