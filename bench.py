@@ -100,7 +100,8 @@ class KernelTimer:
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
-           "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd")
+           "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd", "selunet_bn_bwd_apply_heads",
+           "selunet_bn_bwd_apply_pool")
 
     def __init__(self, esz, tag):
         self.active = False
@@ -206,14 +207,26 @@ class KernelTimer:
             n, h, w, c = (_i(a) for a in args[1:5])
             m = n * h * w
             skip = args[8] is not None and _i(args[8]) != 0
-            return (f"maxpool2_bwd<{t}>", "hbm", 0.0, (2.25 + (1 if skip else 0)) * m * c * esz,
+            wr = args[9] is not None and _i(args[9]) != 0  # (dz null: the BN-backward sums only)
+            return (f"maxpool2_bwd<{t}>", "hbm", 0.0, (1.25 + (1 if wr else 0) + (1 if skip else 0)) * m * c * esz,
                     f"pool bwd {h}x{w} C={c}")
         if name == "selunet_heads_fwd":  # (y, M, sc, sh, w, b, nheads, o0, o1, o2, ...)
             m, nh = _i(args[1]), _i(args[6])
             return f"heads_fwd<{t}>", "hbm", 2.0 * m * 64 * nh, m * 64 * esz + nh * m * 4, "heads fwd"
         if name == "selunet_heads_bwd":  # (y, M, sc, sh, w, nheads, g0, g1, g2, dz, ...)
             m, nh = _i(args[1]), _i(args[5])
-            return f"heads_bwd<{t}>", "hbm", 4.0 * m * 64 * nh, 2 * m * 64 * esz + nh * m * 4, "heads bwd"
+            wr = args[9] is not None and _i(args[9]) != 0  # (dz null: the sums only)
+            return (f"heads_bwd<{t}>", "hbm", 4.0 * m * 64 * nh, (2 if wr else 1) * m * 64 * esz + nh * m * 4,
+                    "heads bwd")
+        if name == "selunet_bn_bwd_apply_heads":  # (y, M, sc, sh, mean, invstd, coef, w, nh, g0, g1, g2, dy, ...)
+            m, nh = _i(args[1]), _i(args[8])
+            return f"bn_bwd_apply<{t}>", "hbm", 0.0, 2 * m * 64 * esz + nh * m * 4, "bn_bwd_apply heads"
+        if name == "selunet_bn_bwd_apply_pool":  # (y, n, h, w, c, sc, sh, mean, invstd, coef, dp, dskip, dy, ...)
+            n, h, w, c = (_i(a) for a in args[1:5])
+            m = n * h * w
+            skip = args[11] is not None and _i(args[11]) != 0
+            return (f"bn_bwd_apply<{t}>", "hbm", 0.0, (2.25 + (1 if skip else 0)) * m * c * esz,
+                    f"bn_bwd_apply pool {h}x{w} C={c}")
         return None
 
     def __call__(self, name, args, fn):

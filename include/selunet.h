@@ -482,7 +482,8 @@ int selunet_maxpool2_fwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t
                          void* stream);
 /* dz = route(dpool to the first max of each window, row-major, strict >) + dskip (nullable).
  * bnb (nullable; bnb->y must be y): BatchNorm-backward sums of dz, slab
- * [selunet_maxpool2_bwd_slab_rows(n, h, w, c)][3][c]. */
+ * [selunet_maxpool2_bwd_slab_rows(n, h, w, c)][3][c]. dz may be NULL when bnb is given: the sums only
+ * (selunet_bn_bwd_apply_pool then forms dz itself). */
 int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
                          const float* scale, const float* shift, const void* dpool,
                          const void* dskip, void* dz, const selunet_bn_bwd_stats* bnb, int32_t dtype,
@@ -500,6 +501,22 @@ int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float*
                       const float* w, int32_t nh, const float* g0, const float* g1,
                       const float* g2, void* dz, float* slab, const selunet_bn_bwd_stats* bnb,
                       int32_t dtype, void* stream);
+/* BatchNorm-backward apply (as selunet_bn_bwd_apply_amax; amax nullable) with dA formed on the fly
+ * instead of read, for the two producers whose dA is cheap to recompute — their kernels then run in
+ * sums-only mode (dz = NULL), so dA is never written:
+ *  _heads: dA[m][c] = sum_h g_h[m] w_h[c] (C = 64; the arguments of selunet_heads_bwd);
+ *  _pool:  dA = route(dpool) + dskip (the arguments of selunet_maxpool2_bwd).
+ * dA is rounded to dtype before use, as the stored tensor of the unfused path. Replaces the
+ * selunet_heads_bwd / selunet_maxpool2_bwd write + selunet_bn_bwd_apply read of dA for decoder_layer_1_1
+ * and encoder_layer_{1,2,3}_2 (model.py:62-66, 31/35/39, the backward of CBR_2D model.py:12-13). */
+int selunet_bn_bwd_apply_heads(const void* y, int64_t m, const float* scale, const float* shift,
+                               const float* mean, const float* invstd, const float* coef,
+                               const float* w, int32_t nh, const float* g0, const float* g1,
+                               const float* g2, void* dy, float* amax, int32_t dtype, void* stream);
+int selunet_bn_bwd_apply_pool(const void* y, int32_t n, int32_t h, int32_t w, int32_t c,
+                              const float* scale, const float* shift, const float* mean,
+                              const float* invstd, const float* coef, const void* dpool,
+                              const void* dskip, void* dy, float* amax, int32_t dtype, void* stream);
 
 /* ---- N-output 1x1 heads (the CE `UNet`, model.py:106-191: conv1x1 64->n_cls, conv_select
  * 64->2, conv_aux 64->n_cls) on relu(bn(y)), C = 64. Output k (k < n <= 8) is an fp32 plane

@@ -130,6 +130,9 @@ SIGNATURES = {
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_amax": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, P, c_int32, P]),
+    "selunet_bn_bwd_apply_heads": (c_int32, [P, c_int64, P, P, P, P, P, P, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_bn_bwd_apply_pool": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, P, P, P, P,
+                                            c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),
     "selunet_maxpool2_fwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
     "selunet_maxpool2_bwd": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P,
@@ -416,6 +419,13 @@ class Plan:
             self._graphs = {}
         except Exception:  # interpreter shutdown
             pass
+
+
+def fused_apply_enabled():
+    """BN-backward apply forming dA on the fly for the heads / max-pool producers
+    (selunet_bn_bwd_apply_heads / _pool, the producers in sums-only mode). SELUNET_FUSED_APPLY=0: the
+    unfused kernels (dA written by the producer, read by selunet_bn_bwd_apply), for A/B runs and tests."""
+    return os.environ.get("SELUNET_FUSED_APPLY", "1") != "0"
 
 
 def graphs_enabled():

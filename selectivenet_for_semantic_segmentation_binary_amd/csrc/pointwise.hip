@@ -810,7 +810,7 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (arg[e] == q) o[e] += g[e];
-      Vec4<T>::store(dz + off[q], o);
+      if (dz) Vec4<T>::store(dz + off[q], o);  // (null: the sums only, selunet_bn_bwd_apply_pool forms dz)
       if (bn_slab) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = to_f(from_f<T>(o[e]));  // as stored
@@ -901,8 +901,8 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     f32x4 z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) z[e] = fmaxf(yv[e] * sc[e] + sh[e], 0.0f);
-    f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];
-    Vec4<T>::store(dz + p * 64 + c, d);
+    f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];  // (as bn_bwd_apply_heads_kernel forms it)
+    if (dz) Vec4<T>::store(dz + p * 64 + c, d);  // (null: the sums only, selunet_bn_bwd_apply_heads forms dz)
     if (bn_slab) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<T>(d[e]));  // as stored
@@ -965,6 +965,149 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     __syncthreads();
   }
   if (bn_slab) channel_block_reduce<3>(bn.acc, 64, bn_slab + (int64_t)blockIdx.x * 3 * 64);
+}
+
+// =========================================================================== BN-backward apply with dA formed
+// on the fly. Two producers of a layer's dA are cheap to recompute: the 1x1 heads' backward (dA = sum_h
+// g_h w_h, three fp32 planes) and the max-pool backward (dA = route(dP) + dskip). Their kernels then run
+// in sums-only mode (dz = null: the BN-backward sums of dA as it would be stored, no write), and the
+// apply forms dA again from (g planes | y, dP, dskip) instead of reading it: the heads path saves dA's
+// write and re-read (2 x M x 64 x esz), the pool path dA's write (its re-read becomes the dskip read).
+// dy = (y sc + sh > 0 ? k0 dA : 0) - b - a y exactly as bn_bwd_apply_kernel, dA rounded to T first (as
+// stored in the unfused path).
+struct ApplyCoef {
+  f32x4 sc, sh, k0, a, b;
+};
+__device__ inline ApplyCoef apply_coef(const float* scale, const float* shift, const float* mean, const float* invstd,
+                                       const float* coef, int C, int c) {
+  ApplyCoef q;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    q.sc[e] = scale[c + e];
+    q.sh[e] = shift[c + e];
+    q.k0[e] = coef[c + e];
+    const float k2i = coef[2 * C + c + e] * invstd[c + e];
+    q.a[e] = k2i;
+    q.b[e] = coef[C + c + e] - k2i * mean[c + e];
+  }
+  return q;
+}
+__device__ inline f32x4 apply4(const ApplyCoef& q, const f32x4& y, const f32x4& g) {
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (y[e] * q.sc[e] + q.sh[e] > 0.0f ? q.k0[e] * g[e] : 0.0f) - q.b[e] - q.a[e] * y[e];
+  return o;
+}
+template <typename T>
+__device__ inline f32x4 as_stored(f32x4 v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = to_f(from_f<T>(v[e]));
+  return v;
+}
+
+// heads (C = 64): 16 lanes per pixel, 4 channels per lane, HU pixels per lane group in flight
+template <typename T>
+__global__ void bn_bwd_apply_heads_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                          const float* __restrict__ shift, const float* __restrict__ mean,
+                                          const float* __restrict__ invstd, const float* __restrict__ coef,
+                                          const float* __restrict__ w, int nh, const float* __restrict__ g0,
+                                          const float* __restrict__ g1, const float* __restrict__ g2,
+                                          T* __restrict__ dy, float* amax) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const ApplyCoef q = apply_coef(scale, shift, mean, invstd, coef, 64, c);
+  f32x4 wv[3];
+  for (int h = 0; h < 3; ++h) wv[h] = h < nh ? *reinterpret_cast<const f32x4*>(w + h * 64 + c) : f32x4{0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 4);
+  float am = 0.0f;
+  auto one = [&](const f32x4& yv, const float* g, int64_t p) {
+    const f32x4 d = as_stored<T>(wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2]);
+    const f32x4 o = apply4(q, yv, d);
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(o[e]));
+    }
+    Vec4<T>::store(dy + p * 64 + c, o);
+  };
+  int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4);
+  for (; p + (HU - 1) * stride < m; p += HU * stride) {
+    f32x4 yv[HU];
+    float g[HU][3];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int64_t r = p + u * stride;
+      yv[u] = Vec4<T>::load(y + r * 64 + c);
+      g[u][0] = g0[r];
+      g[u][1] = nh > 1 ? g1[r] : 0.0f;
+      g[u][2] = nh > 1 ? g2[r] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) one(yv[u], g[u], p + u * stride);
+  }
+  for (; p < m; p += stride) {
+    const float g[3] = {g0[p], nh > 1 ? g1[p] : 0.0f, nh > 1 ? g2[p] : 0.0f};
+    one(Vec4<T>::load(y + p * 64 + c), g, p);
+  }
+  __shared__ float wred[TPB / 64];
+  if (amax) block_amax(amax, am, wred);
+}
+
+// max-pool: one 2x2 window x 4 channels per thread and iteration (maxpool_bwd_kernel's decomposition; each
+// thread keeps one channel group, the grid stride is a multiple of C/4)
+template <typename T>
+__global__ void bn_bwd_apply_pool_kernel(const T* __restrict__ y, int n, int h, int w, int C,
+                                         const float* __restrict__ scale, const float* __restrict__ shift,
+                                         const float* __restrict__ mean, const float* __restrict__ invstd,
+                                         const float* __restrict__ coef, const T* __restrict__ dp,
+                                         const T* __restrict__ dskip, T* __restrict__ dy, float* amax) {
+  const int ho = h >> 1, wo = w >> 1;
+  const int CG = C >> 2;
+  const int64_t nv = (int64_t)n * ho * wo * CG;
+  const int c = (int)(threadIdx.x % CG) * 4;
+  const ApplyCoef q = apply_coef(scale, shift, mean, invstd, coef, C, c);
+  float am = 0.0f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned p = (unsigned)(i / CG);  // output pixel (< 2^31: checked on the host)
+    const unsigned xo = p % (unsigned)wo, t = p / (unsigned)wo;
+    const unsigned yo = t % (unsigned)ho, img = t / (unsigned)ho;
+    const int64_t base = (((int64_t)img * h + 2 * yo) * w + 2 * xo) * C + c;
+    const int64_t off[4] = {base, base + C, base + (int64_t)w * C, base + (int64_t)w * C + C};
+    f32x4 yr[4], sk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      yr[k] = Vec4<T>::load(y + off[k]);
+      sk[k] = dskip ? Vec4<T>::load(dskip + off[k]) : f32x4{0, 0, 0, 0};
+    }
+    const f32x4 g = Vec4<T>::load(dp + i * 4);
+    int arg[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float best = fmaxf(yr[0][e] * q.sc[e] + q.sh[e], 0.0f);
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float v = fmaxf(yr[k][e] * q.sc[e] + q.sh[e], 0.0f);
+        if (v > best) {  // first maximum in row-major window order (ATen, strict >), as maxpool_bwd_kernel
+          best = v;
+          arg[e] = k;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 d = sk[k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (arg[e] == k) d[e] += g[e];
+      const f32x4 o = apply4(q, yr[k], as_stored<T>(d));
+      if (amax) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(o[e]));
+      }
+      Vec4<T>::store(dy + off[k], o);
+    }
+  }
+  __shared__ float wred[TPB / 64];
+  if (amax) block_amax(amax, am, wred);
 }
 
 // =========================================================================== losses
@@ -1708,7 +1851,8 @@ int64_t selunet_maxpool2_bwd_slab_rows(int32_t n, int32_t h, int32_t w, int32_t 
 int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,
                          const float* shift, const void* dpool, const void* dskip, void* dz,
                          const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream) {
-  SELUNET_REQUIRE(y && dpool && dz && scale && shift && n > 0 && h % 2 == 0 && w % 2 == 0 && ok_channels(c),
+  SELUNET_REQUIRE(y && dpool && (dz || (bnb && bnb->slab)) && scale && shift && n > 0 && h % 2 == 0 && w % 2 == 0 &&
+                      ok_channels(c),
                   "maxpool2_bwd: bad arguments");
   SELUNET_REQUIRE((int64_t)n * (h / 2) * (w / 2) < (int64_t(1) << 31), "maxpool2_bwd: grid too large");
   const float *mean = nullptr, *invstd = nullptr;
@@ -1738,7 +1882,7 @@ int selunet_heads_fwd(const void* y, int64_t m, const float* scale, const float*
 int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float* shift, const float* w, int32_t nh,
                       const float* g0, const float* g1, const float* g2, void* dz, float* slab,
                       const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream) {
-  SELUNET_REQUIRE(y && scale && shift && w && g0 && dz && slab && m > 0 && (nh == 1 || nh == 3),
+  SELUNET_REQUIRE(y && scale && shift && w && g0 && (dz || (bnb && bnb->slab)) && slab && m > 0 && (nh == 1 || nh == 3),
                   "heads_bwd: bad arguments");
   SELUNET_REQUIRE(nh == 1 || (g1 && g2), "heads_bwd: g1/g2 required for 3 heads");
   const float *mean = nullptr, *invstd = nullptr;
@@ -1754,6 +1898,33 @@ int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float*
                                        as_stream(stream), (const T*)y, m, scale, shift, w, nh, g0, g1, g2, (T*)dz,
                                        slab, mean, invstd, bslab));
   return check_launch("heads_bwd");
+}
+
+int selunet_bn_bwd_apply_heads(const void* y, int64_t m, const float* scale, const float* shift, const float* mean,
+                               const float* invstd, const float* coef, const float* w, int32_t nh, const float* g0,
+                               const float* g1, const float* g2, void* dy, float* amax, int32_t dtype, void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && mean && invstd && coef && w && g0 && dy && m > 0 && (nh == 1 || nh == 3),
+                  "bn_bwd_apply_heads: bad arguments");
+  SELUNET_REQUIRE(nh == 1 || (g1 && g2), "bn_bwd_apply_heads: g1/g2 required for 3 heads");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_heads_kernel<T>, dim3(grid_for(m * 16 / HU, 2048)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, mean, invstd, coef, w, nh, g0,
+                                       g1, g2, (T*)dy, amax));
+  return check_launch("bn_bwd_apply_heads");
+}
+
+int selunet_bn_bwd_apply_pool(const void* y, int32_t n, int32_t h, int32_t w, int32_t c, const float* scale,
+                              const float* shift, const float* mean, const float* invstd, const float* coef,
+                              const void* dpool, const void* dskip, void* dy, float* amax, int32_t dtype,
+                              void* stream) {
+  SELUNET_REQUIRE(y && dpool && dy && scale && shift && mean && invstd && coef && n > 0 && h % 2 == 0 && w % 2 == 0 &&
+                      ok_channels(c),
+                  "bn_bwd_apply_pool: bad arguments");
+  SELUNET_REQUIRE((int64_t)n * (h / 2) * (w / 2) < (int64_t(1) << 31), "bn_bwd_apply_pool: grid too large");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_pool_kernel<T>,
+                                       dim3((unsigned)selunet_maxpool2_bwd_slab_rows(n, h, w, c)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, n, h, w, c, scale, shift, mean, invstd, coef,
+                                       (const T*)dpool, (const T*)dskip, (T*)dy, amax));
+  return check_launch("bn_bwd_apply_pool");
 }
 
 int64_t selunet_loss_slab_rows(int64_t p) { return loss_slab_rows(p); }

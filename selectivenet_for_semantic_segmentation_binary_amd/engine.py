@@ -81,10 +81,13 @@ class WPack:
 class DGrad:
     """A data gradient plus the per-workgroup partial sums its producing kernel wrote alongside:
     BN-backward sums [rows][3][C] for a CBR block's dA, or column sums [rows][C] for the up-sampled
-    half of a torch.cat gradient (the ConvTranspose2d bias gradient)."""
+    half of a torch.cat gradient (the ConvTranspose2d bias gradient). `apply` (optional) replaces dA for
+    a producer that ran in sums-only mode (t is None): apply(dy, coef, amax_word_or_None) enqueues the
+    BN-backward apply that forms dA on the fly (selunet_bn_bwd_apply_heads / _pool)."""
     t: torch.Tensor
     slab: torch.Tensor = None
     rows: int = 0
+    apply: object = None
 
 
 def bnb_for(st: BNState, slab) -> K.BnBwdStats:
@@ -607,7 +610,9 @@ class Engine:
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
         wp = ctx.wpack[name]
         dyw = self._word(ctx, "dy:" + name) if wp.mode in X2_MODES else None
-        if dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
+        if dg.apply is not None:  # dA formed on the fly from its producer's inputs
+            dg.apply(dy, coef, dyw)
+        elif dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
             K.call("selunet_bn_bwd_apply_amax", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
                    K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.code, self.stream)
         else:
@@ -681,10 +686,19 @@ class Engine:
         return DGrad(dz, slab, rows)
 
     def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
-        dz = K.keep(torch.empty_like(st.y))
         rows = K.query("selunet_maxpool2_bwd_slab_rows", st.n, st.h, st.w, st.c)
-        slab = K.keep(torch.empty(rows, 3, st.c, dtype=torch.float32, device=dz.device))
+        slab = K.keep(torch.empty(rows, 3, st.c, dtype=torch.float32, device=st.y.device))
         bnb = bnb_for(st, slab)
+        if K.fused_apply_enabled():  # the sums only; the layer's BN-backward apply routes dP itself
+            K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
+                   K.ptr(dp.t), K.ptr(dskip), None, bnb, self.code, self.stream)
+
+            def apply(dy, coef, word):
+                K.call("selunet_bn_bwd_apply_pool", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale),
+                       K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dp.t), K.ptr(dskip),
+                       K.ptr(dy), K.ptr(word), self.code, self.stream)
+            return DGrad(None, slab, rows, apply)
+        dz = K.keep(torch.empty_like(st.y))
         K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(dp.t), K.ptr(dskip), K.ptr(dz), bnb, self.code, self.stream)
         return DGrad(dz, slab, rows)
@@ -724,7 +738,6 @@ class Engine:
         bn = ctx.bn
         heads = LY.HEADS if ctx.selective else LY.HEADS[:1]
         d11 = bn["decoder_layer_1_1"]
-        dz = K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
         rows = K.query("selunet_channel_slab_rows", M)
         bslab = K.keep(torch.empty(rows, 3, 64, dtype=torch.float32, device=dev))
         ce = getattr(ctx, "ce_heads", None)
@@ -734,6 +747,7 @@ class Engine:
                   for g, (_, c) in zip(g_heads, ce)]
             planes = self._planes(gs, ce, H * W, with_slab=True)
             slab = K.keep(torch.empty(rows, planes.row_len, dtype=torch.float32, device=dev))
+            dz = K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
             K.call("selunet_heads_bwd_planes", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w),
                    planes, K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code, self.stream)
             seg = planes.row_len
@@ -743,11 +757,21 @@ class Engine:
             gs = gs + [None] * (3 - len(gs))
             nh = len(heads)
             slab = K.keep(torch.empty(rows, nh * 65, dtype=torch.float32, device=dev))
+            fused = K.fused_apply_enabled()  # sums only: decoder_layer_1_1's apply forms dA from the g planes
+            dz = None if fused else K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
             K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
                    K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
                    self.stream)
             seg = nh * 65
-        dz = DGrad(dz, bslab, rows)
+        apply = None
+        if dz is None:
+            head_w = ctx.head_w
+
+            def apply(dy, coef, word):
+                K.call("selunet_bn_bwd_apply_heads", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift),
+                       K.ptr(d11.mean), K.ptr(d11.invstd), K.ptr(coef), K.ptr(head_w), nh, K.ptr(gs[0]), K.ptr(gs[1]),
+                       K.ptr(gs[2]), K.ptr(dy), K.ptr(word), self.code, self.stream)
+        dz = DGrad(dz, bslab, rows, apply)
         # the head weight/bias grads are one consecutive segment of the gradient buffer (registration
         # order conv1x1, conv_select, conv_aux; weight then bias each): reduce straight into it
         hw0 = G[f"{heads[0]}.weight"]

@@ -1,0 +1,98 @@
+"""BatchNorm-backward apply with dA formed on the fly (selunet_bn_bwd_apply_heads / _pool) against the
+unfused pair it replaces: the producer writing dA (selunet_heads_bwd / selunet_maxpool2_bwd) and
+selunet_bn_bwd_apply_amax reading it. The producers' sums-only mode (dz = NULL) must write the same
+BN-backward and head-weight sums, and the fused apply the same dy and range word, bit for bit (same
+arithmetic, dA rounded to the tensor dtype as stored) — in fp32 and bf16."""
+import pytest
+import torch
+
+from selectivenet_for_semantic_segmentation_binary_amd import _lib as K
+from tests.test_gpu_kernels import gen
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def coefs(c, seed):
+    sc, sh = (gen(c, seed=seed).abs() + 0.5).to(DEV), (gen(c, seed=seed + 1) * 0.3).to(DEV)
+    mean, invstd = (gen(c, seed=seed + 2) * 0.1).to(DEV), (gen(c, seed=seed + 3).abs() + 0.5).to(DEV)
+    coef = (gen(3, c, seed=seed + 4) * 0.5).to(DEV).contiguous()
+    return sc, sh, mean, invstd, coef
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nh", [1, 3])
+def test_apply_heads_equals_unfused(dt, nh):
+    m = 3 * 4096 + 77  # ragged tail
+    code = K.dtype_code(dt)
+    y = gen(m, 64, seed=1).to(dt).to(DEV)
+    sc, sh, mean, invstd, coef = coefs(64, 10)
+    w = (gen(3, 64, seed=2) * 0.2).to(DEV).contiguous()
+    g = [(gen(m, seed=3 + i) * 1e-3).to(DEV) for i in range(3)]
+    gp = [K.ptr(g[i]) if i < nh else None for i in range(3)]
+    rows = K.query("selunet_channel_slab_rows", m)
+    res = []
+    for fused in (False, True):
+        slab = torch.full((rows, nh * 65), float("nan"), device=DEV)
+        bslab = torch.full((rows, 3, 64), float("nan"), device=DEV)
+        bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(bslab))
+        dz = None if fused else torch.empty(m, 64, dtype=dt, device=DEV)
+        K.call("selunet_heads_bwd", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(w), nh, *gp, K.ptr(dz), K.ptr(slab), bnb,
+               code, K.stream_ptr())
+        dy = torch.empty(m, 64, dtype=dt, device=DEV)
+        am = torch.zeros(1, device=DEV)
+        if fused:
+            K.call("selunet_bn_bwd_apply_heads", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+                   K.ptr(coef), K.ptr(w), nh, *gp, K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        else:
+            K.call("selunet_bn_bwd_apply_amax", K.ptr(dz), K.ptr(y), m, 64, K.ptr(sc), K.ptr(sh), K.ptr(mean),
+                   K.ptr(invstd), K.ptr(coef), K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        torch.cuda.synchronize()
+        res.append((slab.cpu(), bslab.cpu(), dy.float().cpu(), am.item()))
+    (s0, b0, d0, a0), (s1, b1, d1, a1) = res
+    assert torch.equal(s0, s1) and torch.equal(b0, b1)
+    assert torch.equal(d0, d1)
+    assert a0 == a1 and (dt != torch.float32 or a0 == d0.abs().max().item())  # (the word is max|dy| before rounding)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c,skip", [(64, True), (128, True), (256, False)])
+def test_apply_pool_equals_unfused(dt, c, skip):
+    n, h, w = 2, 18, 36
+    code = K.dtype_code(dt)
+    m = n * h * w
+    y = ((gen(m, c, seed=21) * 2).round() / 2).to(dt).to(DEV)  # coarse values: ties inside the windows
+    sc, sh, mean, invstd, coef = coefs(c, 30)
+    dp = (gen(m // 4, c, seed=22) * 1e-2).to(dt).to(DEV)
+    ds = (gen(m, c, seed=23) * 1e-2).to(dt).to(DEV) if skip else None
+    rows = K.query("selunet_maxpool2_bwd_slab_rows", n, h, w, c)
+    res = []
+    for fused in (False, True):
+        bslab = torch.full((rows, 3, c), float("nan"), device=DEV)
+        bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(bslab))
+        dz = None if fused else torch.empty(m, c, dtype=dt, device=DEV)
+        K.call("selunet_maxpool2_bwd", K.ptr(y), n, h, w, c, K.ptr(sc), K.ptr(sh), K.ptr(dp), K.ptr(ds), K.ptr(dz),
+               bnb, code, K.stream_ptr())
+        dy = torch.empty(m, c, dtype=dt, device=DEV)
+        am = torch.zeros(1, device=DEV)
+        if fused:
+            K.call("selunet_bn_bwd_apply_pool", K.ptr(y), n, h, w, c, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+                   K.ptr(coef), K.ptr(dp), K.ptr(ds), K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        else:
+            K.call("selunet_bn_bwd_apply_amax", K.ptr(dz), K.ptr(y), m, c, K.ptr(sc), K.ptr(sh), K.ptr(mean),
+                   K.ptr(invstd), K.ptr(coef), K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        torch.cuda.synchronize()
+        res.append((bslab.cpu(), dy.float().cpu(), am.item()))
+    (b0, d0, a0), (b1, d1, a1) = res
+    assert torch.equal(b0, b1)
+    assert torch.equal(d0, d1)
+    assert a0 == a1 and (dt != torch.float32 or a0 == d0.abs().max().item())  # (the word is max|dy| before rounding)
+
+
+def test_sums_only_needs_the_sums():
+    """dz = NULL without a BN-backward slab would compute nothing: refused on the host."""
+    y = torch.zeros(64, 64, device=DEV)
+    sc = torch.ones(64, device=DEV)
+    with pytest.raises(RuntimeError):
+        K.call("selunet_maxpool2_bwd", K.ptr(y), 1, 8, 8, 64, K.ptr(sc), K.ptr(sc), K.ptr(y), None, None, None, K.F32,
+               K.stream_ptr())
