@@ -36,6 +36,7 @@ def main():
             if r.returncode:
                 sys.exit(r.stderr[-4000:])
         objs.append(obj)
+    objs.append(os.path.join(B.BUILD, "build_id.o"))  # (selunet_build_id: the tree's sources; SELUNET_LIB skips the check)
     lib = os.path.join(out, f"libselunet_{name}.so")
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *objs, "-o", lib], check=True)
     print(lib)
