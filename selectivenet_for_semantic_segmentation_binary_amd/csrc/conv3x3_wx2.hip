@@ -75,7 +75,7 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   constexpr int LOW = SMEM_EPI > FLUSH ? SMEM_EPI : FLUSH;  // the epilogue tile / statistics scratch
   constexpr int OFF_RAW = (OFF_B + 2 * BBUF > LOW ? OFF_B + 2 * BBUF : LOW);  // raw halo above both
   constexpr int OFF_SS = OFF_RAW + WX_RAW;
-  constexpr int SMEM = OFF_SS + 2 * WX_CK * 4;
+  constexpr int SMEM = OFF_SS + 4 * WX_CK * 4;  // (coefficients + a sink for the other threads' writes)
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   unsigned char* Vs = smem;
   unsigned char* Bs = smem + OFF_B;
@@ -186,23 +186,18 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
     tile_xy(job / nchunks, img, y0, x0);
     int tq = tid;
     asm volatile("" : "+v"(tq));
+    // branch-free (one basic block with the MFMAs of the step): slices past the halo repeat the last pixel
+    // (the same value its owner writes); without a transform the coefficients are 1 / 0 (coef_load)
+    const float lo = tr && relu ? 0.0f : -__builtin_huge_valf();
 #pragma unroll
     for (int r = 0; r < WX_RAW_ROUNDS; ++r) {
-      const int hidx = r * WX_THREADS + tq;
-      if (hidx >= WX_HPIX * 4) continue;
-      const int hp = hidx >> 2;
+      const int hp = min((r * WX_THREADS + tq) >> 2, WX_HPIX - 1);
       const int hy = hp / WX_HW, hx = hp - hy * WX_HW;
-      f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      if ((unsigned)(y0 - 1 + hy) < (unsigned)g.h && (unsigned)(x0 - 1 + hx) < (unsigned)g.w) {
-        __builtin_memcpy(&v, &rr.v[r], 16);
-        if (tr) {
+      const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)g.h && (unsigned)(x0 - 1 + hx) < (unsigned)g.w;
+      f32x4 v;
+      __builtin_memcpy(&v, &rr.v[r], 16);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float f = v[e] * sc[e] + sh[e];
-            v[e] = relu ? fmaxf(f, 0.0f) : f;
-          }
-        }
-      }
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(v[e] * sc[e] + sh[e], lo) : 0.0f;
       *reinterpret_cast<f32x4*>(Raw + hp * 64 + (tq & 3) * 16) = v;
     }
   };
@@ -239,6 +234,36 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
       }
     }
   };
+
+  auto form_slot = [&](int vb, int s) __attribute__((always_inline)) {
+    const int cg = s & 3, px2 = (s >> 2) & 7, hy = s >> 5;
+    const unsigned char* rp = Raw + (hy * WX_HW + 2 * px2) * 64 + cg * 16;
+    const f32x4 d0 = *reinterpret_cast<const f32x4*>(rp);
+    const f32x4 d1 = *reinterpret_cast<const f32x4*>(rp + 64);
+    const f32x4 d2 = *reinterpret_cast<const f32x4*>(rp + 128);
+    const f32x4 d3 = *reinterpret_cast<const f32x4*>(rp + 192);
+    f32x4 v[4];
+    v[0] = d0 - d2;
+    v[1] = d1 + d2;
+    v[2] = d2 - d1;
+    v[3] = d1 - d3;
+    const int sw = wx_vswz(hy, px2);
+    unsigned char* row = Vs + vb * WX_VBUF + (hy * 8 + px2) * WX_VROW + (cg & 1) * 8;
+#pragma unroll
+    for (int xi = 0; xi < 4; ++xi) {
+      f16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        _Float16 a, b;
+        x2_split(v[xi][e] * xs, a, b);
+        h[e] = a;
+        l[e] = b;
+      }
+      *reinterpret_cast<f16x4*>(row + xi * WX_VPLANE + ((cg >> 1) ^ sw) * 16) = h;
+      *reinterpret_cast<f16x4*>(row + xi * WX_VPLANE + ((2 + (cg >> 1)) ^ sw) * 16) = l;
+    }
+  };
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
 
   // ---------------------------------------------------------------- MFMA step (dy, s)
   int vrow0[MT], vsw0[MT];
@@ -285,8 +310,10 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
   auto coef_load = [&](int job) __attribute__((always_inline)) -> float {
     int c;
     const SrcArg sa = chunk_src(job % nchunks, c);
-    if (tid >= 2 * WX_CK || !sa.scale) return 0.0f;
-    return tid < WX_CK ? sa.scale[c + tid] : sa.shift[c + tid - WX_CK];
+    const bool has = sa.scale != nullptr;
+    const float* p = has ? ((tid & WX_CK) ? sa.shift : sa.scale) + c : wcs;  // (wcs: any valid address)
+    const float v = p[tid & (WX_CK - 1)];
+    return has ? v : ((tid & WX_CK) ? 0.0f : 1.0f);
   };
 
   // ---------------------------------------------------------------- prologue: job 0 -> V buffer 0
@@ -336,18 +363,22 @@ conv3x3_wx2_kernel(GatherArg g, const unsigned char* __restrict__ W, int N, EpiA
         const int st = c * STEPS + t;
         const int st2 = st + 2;
         const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);  // (the next tile's steps wrap)
-        if (t == 0 && has_next && tid < 2 * WX_CK) Ss[tid] = creg;
+        // staging without branches (so the scheduler can place it among the step's MFMAs): past the
+        // last job it stages harmless copies; at a tile's last chunk the V planes / weights it writes are
+        // overwritten by the epilogue and staged again after it (rb_hold, form_v below)
+        if (t == 0) Ss[tid < 2 * WX_CK ? tid : 2 * WX_CK + (tid & (2 * WX_CK - 1))] = creg;
         mma_step(J & 1, S & 1, t);
-        if (t == 2 && has_next) raw_store(ra, J + 1, sn.scale != nullptr, Ss + rcc * 4, Ss + WX_CK + rcc * 4, sn.relu);
-        if (t == 3 && J + 2 < njobs) {
-          ra = raw_load(J + 2);
-          creg = coef_load(J + 2);
+        if (t == 2) raw_store(ra, J + 1, sn.scale != nullptr, Ss + rcc * 4, Ss + WX_CK + rcc * 4, sn.relu);
+        if (t == 3) {
+          const int jn = J + 2 < njobs ? J + 2 : J;
+          ra = raw_load(jn);
+          creg = coef_load(jn);
         }
-        // (slots 0-511 at t = 4, the last 64 — wave 0 — at t = 5)
-        if (t == 4 && has_next && !defer) form_v((J + 1) & 1, 0, WX_THREADS);
-        if (t == 5 && has_next && !defer) form_v((J + 1) & 1, WX_THREADS, WX_SLOTS);
-        if (defer && t == STEPS - 1) rb_hold = rb_next;
-        else b_store(rb_next, (S + 1) & 1);
+        // (slots 0-511 at t = 4, the last 64 — wave 7 — at t = 5)
+        if (t == 4) form_slot((J + 1) & 1, tid);
+        if (t == 5 && wv == 7) form_slot((J + 1) & 1, WX_THREADS + lane);
+        if (t == STEPS - 1) rb_hold = rb_next;
+        b_store(rb_next, (S + 1) & 1);
         __syncthreads();
         rb_next = rb_far;
         ++S;
