@@ -27,7 +27,9 @@ BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 # fp32 BatchNorm statistics: channel groups with mean^2 > BN_CENTER_RATIO x the one-pass variance get
 # the centered second pass over y (selunet_bn_centered_partials_adaptive); None: every channel does
-BN_CENTER_RATIO = None if os.environ.get("SELUNET_BN_TWOPASS", "0") == "1" else 1.0
+# (SELUNET_BN_FLAG_RATIO: the threshold for A/B runs)
+BN_CENTER_RATIO = (None if os.environ.get("SELUNET_BN_TWOPASS", "0") == "1"
+                   else float(os.environ.get("SELUNET_BN_FLAG_RATIO", "1.0")))
 FIRST_KPAD = 32  # packed K of encoder_layer_1_1 (9 * C_in <= 27), see selunet_first_conv_fwd
 
 
