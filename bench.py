@@ -101,7 +101,7 @@ class KernelTimer:
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
            "selunet_maxpool2_bwd", "selunet_heads_fwd", "selunet_heads_bwd", "selunet_bn_bwd_apply_heads",
-           "selunet_bn_bwd_apply_pool")
+           "selunet_bn_bwd_apply_pool", "selunet_bn_bwd_apply_heads_planes")
 
     def __init__(self, esz, tag):
         self.active = False
@@ -221,6 +221,9 @@ class KernelTimer:
         if name == "selunet_bn_bwd_apply_heads":  # (y, M, sc, sh, mean, invstd, coef, w, nh, g0, g1, g2, dy, ...)
             m, nh = _i(args[1]), _i(args[8])
             return f"bn_bwd_apply<{t}>", "hbm", 0.0, 2 * m * 64 * esz + nh * m * 4, "bn_bwd_apply heads"
+        if name == "selunet_bn_bwd_apply_heads_planes":  # (y, M, sc, sh, mean, invstd, coef, w, planes, dy, ...)
+            m, nk = _i(args[1]), int(args[8].n)
+            return f"bn_bwd_apply<{t}>", "hbm", 0.0, 2 * m * 64 * esz + nk * m * 4, "bn_bwd_apply heads planes"
         if name == "selunet_bn_bwd_apply_pool":  # (y, n, h, w, c, sc, sh, mean, invstd, coef, dp, dskip, dy, ...)
             n, h, w, c = (_i(a) for a in args[1:5])
             m = n * h * w

@@ -540,6 +540,12 @@ int selunet_heads_fwd_planes(const void* y, int64_t m, const float* scale, const
 int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const float* shift,
                              const float* w, const selunet_head_planes* grads, void* dz, float* slab,
                              const selunet_bn_bwd_stats* bnb, int32_t dtype, void* stream);
+/* selunet_bn_bwd_apply_heads for the N-output heads: dA[m][c] = sum_k g_k[m] w_k[c] from the gradient
+ * planes of selunet_heads_bwd_planes (which then runs with dz = NULL: the sums only). */
+int selunet_bn_bwd_apply_heads_planes(const void* y, int64_t m, const float* scale, const float* shift,
+                                      const float* mean, const float* invstd, const float* coef,
+                                      const float* w, const selunet_head_planes* grads, void* dy,
+                                      float* amax, int32_t dtype, void* stream);
 
 /* ---- losses ----------------------------------------------------------------------------- */
 /* calc_selective_risk_image_b (selective_loss.py:58-85), numerically stable form.

@@ -131,6 +131,8 @@ SIGNATURES = {
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_amax": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_heads": (c_int32, [P, c_int64, P, P, P, P, P, P, c_int32, P, P, P, P, P, c_int32, P]),
+    "selunet_bn_bwd_apply_heads_planes": (c_int32, [P, c_int64, P, P, P, P, P, P, ctypes.POINTER(HeadPlanes), P, P,
+                                                    c_int32, P]),
     "selunet_bn_bwd_apply_pool": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, P, P, P, P, P, P,
                                             c_int32, P]),
     "selunet_im2col3x3": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, c_int32, P]),

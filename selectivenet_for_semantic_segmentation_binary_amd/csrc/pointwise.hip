@@ -1291,7 +1291,7 @@ __global__ void heads_n_bwd_kernel(const T* __restrict__ y, int64_t m, const flo
         db[k] += g;
       }
     }
-    Vec4<T>::store(dz + p * 64 + c, d);
+    if (dz) Vec4<T>::store(dz + p * 64 + c, d);  // (null: the sums only, selunet_bn_bwd_apply_heads_planes forms dz)
     if (bn_slab) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<T>(d[e]));  // as stored
@@ -1324,6 +1324,42 @@ __global__ void heads_n_bwd_kernel(const T* __restrict__ y, int64_t m, const flo
   }
   if (bn_slab) channel_block_reduce<3>(bn.acc, 64, bn_slab + (int64_t)blockIdx.x * 3 * 64);
 }
+
+// the N-output heads of the CE UNet (up to 8 gradient planes, selunet_head_planes): dA = sum_k g_k w_k,
+// formed in the order of heads_n_bwd_kernel
+template <typename T>
+__global__ void bn_bwd_apply_heads_planes_kernel(const T* __restrict__ y, int64_t m, const float* __restrict__ scale,
+                                                 const float* __restrict__ shift, const float* __restrict__ mean,
+                                                 const float* __restrict__ invstd, const float* __restrict__ coef,
+                                                 const float* __restrict__ w, HeadPlanesArg hp, T* __restrict__ dy,
+                                                 float* amax) {
+  const int sub = threadIdx.x & 15;
+  const int c = sub * 4;
+  const ApplyCoef q = apply_coef(scale, shift, mean, invstd, coef, 64, c);
+  f32x4 wv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) wv[k] = k < hp.n ? *reinterpret_cast<const f32x4*>(w + k * 64 + c) : f32x4{0, 0, 0, 0};
+  float am = 0.0f;
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 4);
+  for (int64_t p = blockIdx.x * (int64_t)(blockDim.x >> 4) + (threadIdx.x >> 4); p < m; p += stride) {
+    const f32x4 yv = Vec4<T>::load(y + p * 64 + c);
+    const int64_t img = p / hp.hw, qq = p - img * hp.hw;
+    f32x4 d = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < hp.n) d += wv[k] * hp.plane[k][img * hp.img_stride[k] + qq];
+    }
+    const f32x4 o = apply4(q, yv, as_stored<T>(d));
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(o[e]));
+    }
+    Vec4<T>::store(dy + p * 64 + c, o);
+  }
+  __shared__ float wred[TPB / 64];
+  if (amax) block_amax(amax, am, wred);
+}
+
 
 // =========================================================================== cross-entropy losses
 // logits NCHW [N][C][hw]; lse over C <= 8 classes (max-shifted), ell = lse - x[t]
@@ -2037,7 +2073,7 @@ int selunet_heads_fwd_planes(const void* y, int64_t m, const float* scale, const
 int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const float* shift, const float* w,
                              const selunet_head_planes* grads, void* dz, float* slab, const selunet_bn_bwd_stats* bnb,
                              int32_t dtype, void* stream) {
-  SELUNET_REQUIRE(y && scale && shift && w && dz && slab && m > 0, "heads_bwd_planes: bad arguments");
+  SELUNET_REQUIRE(y && scale && shift && w && (dz || (bnb && bnb->slab)) && slab && m > 0, "heads_bwd_planes: bad arguments");
   HeadPlanesArg h;
   if (int rc = head_planes_arg(grads, h, true)) return rc;
   SELUNET_REQUIRE(m % h.hw == 0, "heads_bwd_planes: m (%lld) must be a multiple of hw (%d)", (long long)m, h.hw);
@@ -2055,6 +2091,23 @@ int selunet_heads_bwd_planes(const void* y, int64_t m, const float* scale, const
                                        invstd, bslab));
   return check_launch("heads_bwd_planes");
 }
+
+int selunet_bn_bwd_apply_heads_planes(const void* y, int64_t m, const float* scale, const float* shift,
+                                      const float* mean, const float* invstd, const float* coef, const float* w,
+                                      const selunet_head_planes* grads, void* dy, float* amax, int32_t dtype,
+                                      void* stream) {
+  SELUNET_REQUIRE(y && scale && shift && mean && invstd && coef && w && dy && m > 0,
+                  "bn_bwd_apply_heads_planes: bad arguments");
+  HeadPlanesArg h;
+  if (int rc = head_planes_arg(grads, h, true)) return rc;
+  SELUNET_REQUIRE(m % h.hw == 0, "bn_bwd_apply_heads_planes: m (%lld) must be a multiple of hw (%d)", (long long)m,
+                  h.hw);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_heads_planes_kernel<T>, dim3(grid_for(m * 16, 2048)), dim3(TPB), 0,
+                                       as_stream(stream), (const T*)y, m, scale, shift, mean, invstd, coef, w, h,
+                                       (T*)dy, amax));
+  return check_launch("bn_bwd_apply_heads_planes");
+}
+
 
 static int ce_selective_partials(bool hard, const float* out, const float* sel, const int64_t* target, int64_t n,
                                  int32_t c, int64_t hw, float* slab, void* stream) {

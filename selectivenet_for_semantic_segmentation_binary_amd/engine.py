@@ -749,10 +749,17 @@ class Engine:
                   for g, (_, c) in zip(g_heads, ce)]
             planes = self._planes(gs, ce, H * W, with_slab=True)
             slab = K.keep(torch.empty(rows, planes.row_len, dtype=torch.float32, device=dev))
-            dz = K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
+            fused = K.fused_apply_enabled()  # sums only: decoder_layer_1_1's apply forms dA from the planes
+            dz = None if fused else K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
             K.call("selunet_heads_bwd_planes", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w),
                    planes, K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code, self.stream)
             seg = planes.row_len
+            head_w = ctx.head_w
+
+            def apply_planes(dy, coef, word):
+                K.call("selunet_bn_bwd_apply_heads_planes", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift),
+                       K.ptr(d11.mean), K.ptr(d11.invstd), K.ptr(coef), K.ptr(head_w), planes, K.ptr(dy),
+                       K.ptr(word), self.code, self.stream)
         else:
             gs = [g if g is not None else K.keep(torch.zeros(n, H, W, dtype=torch.float32, device=dev))
                   for g in g_heads]
@@ -765,8 +772,8 @@ class Engine:
                    K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
                    self.stream)
             seg = nh * 65
-        apply = None
-        if dz is None:
+        apply = apply_planes if (ce is not None and dz is None) else None
+        if dz is None and ce is None:
             head_w = ctx.head_w
 
             def apply(dy, coef, word):

@@ -89,6 +89,53 @@ def test_apply_pool_equals_unfused(dt, c, skip):
     assert a0 == a1 and (dt != torch.float32 or a0 == d0.abs().max().item())  # (the word is max|dy| before rounding)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_apply_heads_planes_equals_unfused(dt):
+    """The CE UNet's N-output heads (selunet_heads_bwd_planes / selunet_bn_bwd_apply_heads_planes): 2 images,
+    outputs of 2 + 2 + 2 channels as NCHW planes."""
+    n, hw, nk = 2, 48 * 40, 6
+    m = n * hw
+    code = K.dtype_code(dt)
+    y = gen(m, 64, seed=81).to(dt).to(DEV)
+    sc, sh, mean, invstd, coef = coefs(64, 90)
+    w = (gen(8, 64, seed=82) * 0.2).to(DEV).contiguous()
+    g = (gen(3, n, 2, hw, seed=83) * 1e-3).to(DEV).contiguous()  # three [N, 2, H*W] gradient tensors
+    hp = K.HeadPlanes()
+    hp.n, hp.hw = nk, hw
+    row_len = 0
+    for k in range(nk):
+        t, j = divmod(k, 2)
+        hp.plane[k] = g[t].data_ptr() + j * hw * 4
+        hp.img_stride[k] = 2 * hw
+        hp.w_off[k] = k * 65
+        hp.b_off[k] = k * 65 + 64
+        row_len = (k + 1) * 65
+    hp.row_len = row_len
+    rows = K.query("selunet_channel_slab_rows", m)
+    res = []
+    for fused in (False, True):
+        slab = torch.full((rows, row_len), float("nan"), device=DEV)
+        bslab = torch.full((rows, 3, 64), float("nan"), device=DEV)
+        bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(bslab))
+        dz = None if fused else torch.empty(m, 64, dtype=dt, device=DEV)
+        K.call("selunet_heads_bwd_planes", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(w), hp, K.ptr(dz), K.ptr(slab), bnb,
+               code, K.stream_ptr())
+        dy = torch.empty(m, 64, dtype=dt, device=DEV)
+        am = torch.zeros(1, device=DEV)
+        if fused:
+            K.call("selunet_bn_bwd_apply_heads_planes", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+                   K.ptr(coef), K.ptr(w), hp, K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        else:
+            K.call("selunet_bn_bwd_apply_amax", K.ptr(dz), K.ptr(y), m, 64, K.ptr(sc), K.ptr(sh), K.ptr(mean),
+                   K.ptr(invstd), K.ptr(coef), K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        torch.cuda.synchronize()
+        res.append((slab.cpu(), bslab.cpu(), dy.float().cpu(), am.item()))
+    (s0, b0, d0, a0), (s1, b1, d1, a1) = res
+    assert torch.equal(s0, s1) and torch.equal(b0, b1)
+    assert torch.equal(d0, d1)
+    assert a0 == a1
+
+
 def test_sums_only_needs_the_sums():
     """dz = NULL without a BN-backward slab would compute nothing: refused on the host."""
     y = torch.zeros(64, 64, device=DEV)
