@@ -48,6 +48,9 @@ for _t in ("bf16", "f32"):
         (_pat("conv3x3_halo_kernel", _t, 64), f"conv3x3_halo<{_t},64>"),
         (_pat("gemm_gather_kernel", _t), f"gemm_gather<{_t}>"),
         (_pat("bn_bwd_apply_kernel", _t), f"bn_bwd_apply<{_t}>"),
+        (_pat("bn_bwd_apply_pool_kernel", _t), f"bn_bwd_apply<{_t}>"),  # (dA formed on the fly: same entry in bench.py)
+        (_pat("bn_bwd_apply_heads_kernel", _t), f"bn_bwd_apply<{_t}>"),
+        (_pat("bn_bwd_apply_heads_planes_kernel", _t), f"bn_bwd_apply<{_t}>"),
         (_pat("maxpool_fwd_kernel", _t), f"maxpool2_fwd<{_t}>"),
         (_pat("maxpool_bwd_kernel", _t), f"maxpool2_bwd<{_t}>"),
         (_pat("heads_fwd_kernel", _t), f"heads_fwd<{_t}>"),
