@@ -682,25 +682,29 @@ __device__ __forceinline__ uint4 gather_vec8_bf16(const GatherArg& g, int64_t m,
   return raw;
 }
 
-template <int BI, int BJ, bool SMALL>
-__global__ void __launch_bounds__(256, 2)
+// NTH = 512 (round 4): 256-column tiles on 8 waves (2 x 4), one workgroup per CU, as gemm_wgrad_x2_kernel —
+// the ConvTranspose2d weight gradients re-read each operand once per tile of the other
+template <int BI, int BJ, bool SMALL, int NTH = 256>
+__global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1)
 gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ldo, int64_t mchunk, int tiles_j,
                        int tiles, float* __restrict__ ws, int64_t ws_stride) {
   constexpr int KM = 64;                           // pixels per stage
   constexpr int PADE = 32;                         // 64 B row pad (bank spread for tr reads)
   constexpr int LDI = BI + PADE, LDJ = BJ + PADE;  // row strides in elements
-  constexpr int WI = BI / 2, WJ = BJ / 2;
+  constexpr int WGJ = NTH / 128;                   // waves along j (2 along i)
+  constexpr int WI = BI / 2, WJ = BJ / WGJ;
   constexpr int MT = WI / 32, NT = WJ / 32;
   constexpr int CPI = BI / 8, CPJ = BJ / 8;        // 16-B chunks per row
-  constexpr int RPI = 256 / CPI, RPJ = 256 / CPJ;
+  constexpr int RPI = NTH / CPI, RPJ = NTH / CPJ;
   constexpr int PI = KM / RPI, PJ = KM / RPJ;
+  static_assert(PI >= 1 && PJ >= 1 && MT >= 1 && NT >= 1, "stage rows must cover the threads");
 
   __shared__ __attribute__((aligned(16))) unsigned short Ps[2][KM][LDI];
   __shared__ __attribute__((aligned(16))) unsigned short Qs[2][KM][LDJ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
+  const int wi = wave / WGJ, wj = wave % WGJ;
   const int half = lane >> 5, l32 = lane & 31;
   const int grp_hi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
 
@@ -1349,6 +1353,7 @@ struct WgradPlan {
   bool halo;
   bool wino;       // fp32 Winograd planes (split-partials paths only): ws row length 12 * C
   int64_t splits;  // pixel splits whose partials the fixed-order reduction sums
+  int wide_bi;     // bf16 generic path on 256-column tiles (512 threads, one workgroup per CU): 256 / 128, or 0
 };
 
 static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t dtype, WgradPlan& w) {
@@ -1360,6 +1365,7 @@ static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t 
   SELUNET_REQUIRE(w.gp.K % 64 == 0, "P columns (%d) must be a multiple of 64", w.gp.K);
   SELUNET_REQUIRE(w.gp.small == 0, "P must be vector-gatherable");
   w.ni = w.gp.K;
+  w.wide_bi = 0;
   w.bj = (w.gq.K % 128 == 0 || w.gq.K > 512) ? 128 : 64;
   w.nj_pad = (int)(cdiv(w.gq.K, w.bj) * w.bj);
   w.halo = halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, dtype);
@@ -1369,6 +1375,14 @@ static int plan_wgrad(const selunet_gather* p, const selunet_gather* q, int32_t 
   } else if (w.halo) {
     w.splits = conv3x3_wgrad_halo_splits(w.gp, w.gq, dtype, nullptr);
   } else {
+    // bf16, vector operands, 256-column tiles possible (the ConvTranspose2d weight gradients): 256 x 256 or
+    // 128 x 256 tiles, pixel splits sized for 256 workgroups (gemm_wgrad_x2's tiling)
+    if (dtype == SELUNET_BF16 && !w.gp.small && !w.gq.small && w.gq.K % 256 == 0 && (w.ni % 256 == 0 || w.ni == 128)) {
+      w.wide_bi = w.ni % 256 == 0 ? 256 : 128;
+      w.nj_pad = w.gq.K;
+      w.splits = wgrad_splits(w.gp.M, (w.ni / w.wide_bi) * (w.nj_pad / 256), nullptr, 256);
+      return 0;
+    }
     const int bi = w.ni % 128 == 0 ? 128 : 64;
     w.splits = wgrad_splits(w.gp.M, (w.ni / bi) * (w.nj_pad / w.bj), nullptr);
   }
@@ -1399,6 +1413,19 @@ static void launch_wgrad_any(const WgradPlan& w, float* out, float* ws, int32_t 
     return;
   }
   const bool bi128 = ni % 128 == 0;
+  if (w.wide_bi && ws) {  // bf16 256-column tiles (split partials only)
+    const int tiles_j = nj_pad / 256, tiles = (ni / w.wide_bi) * tiles_j;
+    int64_t mchunk;
+    const int64_t splits = wgrad_splits(gp.M, tiles, &mchunk, 256);
+    const dim3 grid((unsigned)(tiles * splits));
+    if (w.wide_bi == 256)
+      hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<256, 256, false, 512>), grid, dim3(512), 0, st, gp, gq, out, nj_pad,
+                         mchunk, tiles_j, tiles, ws, (int64_t)ni * nj_pad);
+    else
+      hipLaunchKernelGGL((gemm_wgrad_bf16_kernel<128, 256, false, 512>), grid, dim3(512), 0, st, gp, gq, out, nj_pad,
+                         mchunk, tiles_j, tiles, ws, (int64_t)ni * nj_pad);
+    return;
+  }
   // out is [ni][nj_pad] where nj_pad = roundup(Kq, 64 or 128): see selunet_wgrad_ld()
   if (dtype == SELUNET_F32) {
     if (bi128 && bj == 128) launch_wgrad<float, 128, 128>(gp, gq, out, nj_pad, ni, nj_pad, st, ws);
