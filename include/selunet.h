@@ -52,7 +52,7 @@ enum {
   SELUNET_OPT_GEMM_WGRAD_WGS,     /* workgroup target of the generic weight gradient (512) */
   SELUNET_OPT_GATHER_WGS,         /* resident gather-GEMM workgroups (512; 0 = one tile each) */
   SELUNET_OPT_RF_SINGLE,          /* slab rows reduced in one launch by the fused reductions (1024) */
-  SELUNET_OPT_APPLY_U8,           /* BN-backward apply: 8 channel groups per thread (0) */
+  SELUNET_OPT_APPLY_U8,           /* BN-backward apply form: 0 8 ch x 4 px, 1 8 ch x 8 px, 2/3 4 contiguous ch x 8/16 px (0) */
   SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
   SELUNET_OPT_WX2,                /* selunet_conv3x3_wx2_ok admits layers to the split-fp16 Winograd kernel (0:
                                    * measured slower than selunet_conv3x3_x2 on every UNet_B layer) */

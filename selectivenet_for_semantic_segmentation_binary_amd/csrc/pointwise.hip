@@ -650,6 +650,57 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restric
   if (amax) block_amax(amax, am, wred);
 }
 
+// The same with 4 channels per thread, lanes of a wave on consecutive 16-B (fp32) vectors: C / 4 lanes per
+// pixel, so each load / store instruction covers 64 x 16 contiguous bytes (the 8-channel form above
+// reads two interleaved halves of every 32-B segment per instruction); U pixels per thread in flight.
+template <typename T, int U>
+__global__ void bn_bwd_apply4_kernel(const T* __restrict__ dz, const T* __restrict__ y, int64_t m, int C,
+                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                     const float* __restrict__ mean, const float* __restrict__ invstd,
+                                     const float* __restrict__ coef, T* __restrict__ dy, float* amax) {
+  const int CG = C >> 2;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
+  const int PL = TPB / CG;
+  const int c = cg * 4;
+  float sc[4], sh[4], k0[4], a[4], b[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = scale[c + e];
+    sh[e] = shift[c + e];
+    k0[e] = coef[c + e];
+    const float k2i = coef[2 * C + c + e] * invstd[c + e];
+    a[e] = k2i;
+    b[e] = coef[C + c + e] - k2i * mean[c + e];
+  }
+  const int64_t stride = (int64_t)gridDim.x * PL;
+  float am = 0.0f;
+  auto one = [&](const f32x4& yv, const f32x4& g, int64_t off) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (yv[e] * sc[e] + sh[e] > 0.0f ? k0[e] * g[e] : 0.0f) - b[e] - a[e] * yv[e];
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(o[e]));
+    }
+    Vec4<T>::store(dy + off, o);
+  };
+  int64_t p = blockIdx.x * (int64_t)PL + pl;
+  for (; p + (U - 1) * stride < m; p += U * stride) {
+    f32x4 yv[U], g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (p + u * stride) * C + c;
+      yv[u] = Vec4<T>::load(y + off);
+      g[u] = Vec4<T>::load(dz + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(yv[u], g[u], (p + u * stride) * C + c);
+  }
+  for (; p < m; p += stride) one(Vec4<T>::load(y + p * C + c), Vec4<T>::load(dz + p * C + c), p * C + c);
+  __shared__ float wred[TPB / 64];
+  if (amax) block_amax(amax, am, wred);
+}
+
 // selunet_act_bound: max_c |gamma_c| * sqrt(count) + max_c |beta_c| (one block)
 __global__ void __launch_bounds__(256) act_bound_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         int C, float sq, float* out) {
@@ -1849,8 +1900,22 @@ int selunet_bn_bwd_apply_amax(const void* dz, const void* y, int64_t m, int32_t 
   SELUNET_REQUIRE(dz && y && scale && shift && mean && invstd && coef && dy && m > 0 && c % 4 == 0,
                   "bn_bwd_apply: bad arguments");
   SELUNET_REQUIRE(ok_channels(c), "bn_bwd_apply: C must be 64, 128, 256 or 512 (got %d)", c);
-  const bool u8 = option(SELUNET_OPT_APPLY_U8, 0) != 0;
+  const int64_t form = option(SELUNET_OPT_APPLY_U8, 0);  // 0: 8 channels x 4 pixels, 1: x 8 pixels, 2 / 3: the
+                                                           // 4-channel contiguous form with 8 / 16 pixels in flight
+  const bool u8 = form == 1;
   const int64_t gcap = std::max<int64_t>(1, option(SELUNET_OPT_APPLY_GRID, 1024));
+  if (form == 2 || form == 3) {
+    const unsigned b4 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 4)), gcap));
+    if (form == 2)
+      DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply4_kernel<T, 8>), dim3(b4), dim3(TPB), 0, as_stream(stream),
+                                           (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd, coef, (T*)dy,
+                                           amax));
+    else
+      DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply4_kernel<T, 16>), dim3(b4), dim3(TPB), 0, as_stream(stream),
+                                           (const T*)dz, (const T*)y, m, c, scale, shift, mean, invstd, coef, (T*)dy,
+                                           amax));
+    return check_launch("bn_bwd_apply");
+  }
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(m, TPB / (c / 8)), gcap));
   if (u8) {
     DISPATCH_T(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(blocks), dim3(TPB), 0, as_stream(stream),

@@ -136,6 +136,30 @@ def test_apply_heads_planes_equals_unfused(dt):
     assert a0 == a1
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c", [64, 128, 256, 512])
+@pytest.mark.parametrize("form", [1, 2, 3])
+def test_apply_forms_equal(dt, c, form):
+    """The apply kernel's alternative forms (SELUNET_OPT_APPLY_U8: 8 channels x 8 pixels, 4 contiguous
+    channels x 8 / 16 pixels) against the default form, bit for bit, ragged pixel count."""
+    m = 4096 * 3 + 5
+    code = K.dtype_code(dt)
+    y = gen(m, c, seed=41).to(dt).to(DEV)
+    dz = (gen(m, c, seed=42) * 1e-2).to(dt).to(DEV)
+    sc, sh, mean, invstd, coef = coefs(c, 50)
+    res = []
+    for f in (0, form):
+        prev = K.set_option("APPLY_U8", f)
+        dy = torch.full((m, c), float("nan"), dtype=dt, device=DEV)
+        am = torch.zeros(1, device=DEV)
+        K.call("selunet_bn_bwd_apply_amax", K.ptr(dz), K.ptr(y), m, c, K.ptr(sc), K.ptr(sh), K.ptr(mean),
+               K.ptr(invstd), K.ptr(coef), K.ptr(dy), K.ptr(am), code, K.stream_ptr())
+        torch.cuda.synchronize()
+        K.set_option("APPLY_U8", prev)
+        res.append((dy.float().cpu(), am.item()))
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
 def test_sums_only_needs_the_sums():
     """dz = NULL without a BN-backward slab would compute nothing: refused on the host."""
     y = torch.zeros(64, 64, device=DEV)

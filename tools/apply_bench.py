@@ -1,6 +1,8 @@
 """Time selunet_bn_bwd_apply(_amax) at the fp32 shapes of a batch (profiling tool).
 
-    python tools/apply_bench.py [--iters 20] [--batch 128]
+    python tools/apply_bench.py [--iters 20] [--batch 128] [--forms 0,1,2,3] [--grids 1024]
+
+--forms / --grids sweep SELUNET_OPT_APPLY_U8 (the kernel form) and SELUNET_OPT_APPLY_GRID (grid cap).
 """
 import argparse
 import os
@@ -18,7 +20,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--forms", default="0")
+    ap.add_argument("--grids", default="1024")
     a = ap.parse_args()
+    for form in [int(x) for x in a.forms.split(",")]:
+        for grid in [int(x) for x in a.grids.split(",")]:
+            K.set_option("APPLY_U8", form)
+            K.set_option("APPLY_GRID", grid)
+            print(f"form {form} grid {grid}", flush=True)
+            run(a)
+
+
+def run(a):
     tot = 0.0
     for px, c in SHAPES:
         m = a.batch * px
@@ -41,7 +54,7 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / a.iters
         tot += ms
-        print(f"apply m={m:9d} C={c:3d}: {ms:.3f} ms  {3 * m * c * 4 / ms / 1e9:7.1f} GB/s", flush=True)
+        print(f"apply m={m:9d} C={c:3d}: {ms:.3f} ms  {3 * m * c * 4 / ms / 1e9:7.2f} TB/s", flush=True)
     print(f"total {tot:.3f} ms")
 
 
