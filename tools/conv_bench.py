@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--wx2", action="store_true", help="fp32 split-fp16 Winograd F(2,3) (selunet_conv3x3_wx2)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    if a.wino or a.x2 or a.wx2:
+        dt = torch.float32  # (fp32 operands: the kernels read the sources as fp32)
     sel = set(a.layers.split(",")) if a.layers else None
     tot_ms, tot_fl = 0.0, 0.0
     for name, (c0, c1), co, hw in LAYERS:
