@@ -42,7 +42,7 @@ enum {
  * variables; every value < 0 selects the built-in default. Selection options take 0/1. */
 enum {
   SELUNET_OPT_HALO = 0,           /* 3x3 convolutions on the LDS halo kernels (1) or the gather GEMM (0) */
-  SELUNET_OPT_HALO_PERSIST,       /* persistent multi-chunk halo kernel (1) */
+  SELUNET_OPT_HALO_PERSIST,       /* persistent halo kernel: 0 off, 1 multi-chunk layers, 2 single-chunk too (1) */
   SELUNET_OPT_WINO,               /* exact-fp32 3x3 fwd/dgrad as 1-D Winograd F(2,3) (1) or direct (0) */
   SELUNET_OPT_WINO_WGRAD,         /* exact-fp32 3x3 weight gradient as the Winograd transpose (1) */
   SELUNET_OPT_WINO_WGRAD_TW,      /* its tile width: 16 (default) or 8 pixels */

@@ -2105,7 +2105,12 @@ static int PERSIST_WGS = PERSIST_WGS_DEFAULT;  // selunet_set_halo_workgroups
 
 static bool persist_enabled() { return option(SELUNET_OPT_HALO_PERSIST, 1) != 0; }
 
-static bool halo_one_chunk(const GatherArg& g, int dtype) { return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64); }
+// single-chunk layers (C = one 128-B chunk) run the non-persistent ONE_CHUNK kernel (two workgroups per CU),
+// unless SELUNET_OPT_HALO_PERSIST = 2 puts them on the persistent kernel too
+static bool halo_one_chunk(const GatherArg& g, int dtype) {
+  return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64) && option(SELUNET_OPT_HALO_PERSIST, 1) != 2;
+}
+bool conv3x3_halo_one_chunk(const GatherArg& g, int dtype) { return halo_one_chunk(g, dtype); }
 
 // output tiles per workgroup row of the persistent launch (= statistics slab rows): PERSIST_WGS
 // workgroups at 128-column tiles; 64-column tiles (N % 128 != 0 or a split at 64) use twice the
@@ -2130,9 +2135,9 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
   const int n_tiles = N / BN;
   const int64_t blocks = conv3x3_halo_tiles(g) * n_tiles;
-  const bool one = g.Ctot == 128 / (int)sizeof(T);
+  const int dtype = sizeof(T) == 2 ? SELUNET_BF16 : SELUNET_F32;
+  const bool one = halo_one_chunk(g, dtype);
   if (!one && persist_enabled()) {
-    const int dtype = sizeof(T) == 2 ? SELUNET_BF16 : SELUNET_F32;
     const int gp = (int)conv3x3_halo_stats_rows(g, N, dtype);
     hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN, false>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0,
                        st, g, reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
@@ -2217,7 +2222,7 @@ int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st) {
   // single-chunk layers use 64-column tiles: LDS for two workgroups per CU
-  const bool one = g.Ctot == (dtype == SELUNET_F32 ? 32 : 64);
+  const bool one = halo_one_chunk(g, dtype);
   const bool bn128 = !one && N % 128 == 0 && !(ep.mode == SELUNET_EP_SPLIT && ep.split % 128 != 0);
   if (dtype == SELUNET_F32) {
     if (bn128) launch_halo<float, 128>(g, b, N, k_pad, ep, st);

@@ -1016,7 +1016,7 @@ extern "C" const char* selunet_gemm_kernel_name(const selunet_gather* a, const s
     if (make_gather(a, dtype, g, 16 / esz)) return "invalid";
     if (mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) {
       // (SPLIT epilogues in this network split the columns in half: torch.cat of equal halves)
-      const bool one = g.Ctot == (bf ? 64 : 32);  // single channel chunk: 64-column tiles, 2 WG/CU
+      const bool one = conv3x3_halo_one_chunk(g, dtype);  // single channel chunk: 64-column tiles, 2 WG/CU
       const bool bn128 = !one && n_cols % 128 == 0 && !(mode == SELUNET_EP_SPLIT && (n_cols / 2) % 128 != 0);
       if (one) return bf ? "conv3x3_halo1<bf16,64>" : "conv3x3_halo1<f32,64>";
       if (conv3x3_halo_persistent(g, dtype))

@@ -440,6 +440,7 @@ int make_gather(const selunet_gather* a, int dtype, GatherArg& g, int vec_elems)
 bool conv3x3_halo_eligible(const GatherArg& g, int N, int dtype);
 int64_t conv3x3_halo_tiles(const GatherArg& g);
 int64_t conv3x3_halo_stats_rows(const GatherArg& g, int N, int dtype);  // slab rows of the halo epilogue
+bool conv3x3_halo_one_chunk(const GatherArg& g, int dtype);             // single chunk: the ONE_CHUNK kernel
 bool conv3x3_halo_persistent(const GatherArg& g, int dtype);            // multi-chunk: persistent kernel
 int conv3x3_halo_launch(const GatherArg& g, const void* b, int N, int k_pad, const EpiArg& ep, int dtype,
                         hipStream_t st);
