@@ -59,6 +59,7 @@ enum {
   SELUNET_OPT_X2D,                /* 64-column split-fp16 3x3 layers on the two-workgroups-per-CU kernel: 0 never,
                                    * 1 every eligible layer, 2 inputs of at most 64 channels, 3 (default) those of
                                    * them whose source carries a BN+ReLU transform (the forwards) */
+  SELUNET_OPT_BF16_M16,           /* bf16 persistent 3x3 kernel on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0) */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an

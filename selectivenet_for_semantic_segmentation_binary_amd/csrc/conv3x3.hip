@@ -303,7 +303,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
                             int tiles_x, int tiles_y, int ptiles, int gp, const float* __restrict__ wcs,
                             const float* __restrict__ amax0, const float* __restrict__ amax1) {
   static_assert(!X2 || std::is_same<T, float>::value, "split-fp16 form of fp32 operands only");
-  static_assert(!M16 || X2, "16x16x32 form: split-fp16 only");
+  static_assert(!M16 || X2 || std::is_same<T, __bf16>::value, "16x16x32 form: split-fp16 or bf16");
   constexpr int E = 16 / sizeof(T);
   constexpr int CK = 128 / sizeof(T);
   constexpr int WAVES_N = BN / 64;
@@ -449,7 +449,26 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     const unsigned char* b_src = Bs + bbuf * BN * WROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
-    if constexpr (M16) {
+    if constexpr (M16 && !X2) {
+      // bf16: a tap's 64-channel chunk as two 16x16x32 k-steps (16-B units 0-3, 4-7 of the 128-B rows);
+      // per k-step the wave's 4 column subtiles' weight fragments, then per tile row its halo fragment
+      // and 4 MFMAs (unit ^ halo-row parity undoes the halo swizzle of halo_store)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 bw[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          bw[b] = *reinterpret_cast<const bf16x8*>(b_src + (wn * 64 + b * 16 + l16) * WROWB + (ks * 4 + kg) * 16);
+#pragma unroll
+        for (int a = 0; a < RT; ++a) {
+          const int py = wm * RT + a;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+              a_src + ((py + dy) * HWT + l16 + dx) * AROWB + (((ks * 4 + kg) ^ ((py + dy) & 1)) << 4));
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[b], acc[a][b], 0, 0, 0);
+        }
+      }
+    } else if constexpr (M16) {
       // the wave's 4 column subtiles' weight fragments (high, low), then per tile row its halo
       // fragments and 12 MFMAs; unit kg ^ (halo row parity) undoes the halo swizzle (halo_store)
       f16x8 bh[4], bl[4];
@@ -2139,9 +2158,12 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   const bool one = halo_one_chunk(g, dtype);
   if (!one && persist_enabled()) {
     const int gp = (int)conv3x3_halo_stats_rows(g, N, dtype);
-    hipLaunchKernelGGL((conv3x3_halo_persist_kernel<T, BN, false>), dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0,
-                       st, g, reinterpret_cast<const T*>(b), N, k_pad, ep, n_tiles, tiles_x, tiles_y,
-                       (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr);
+    // bf16: 16x16x32 MFMAs (SELUNET_OPT_BF16_M16; 160-B weight rows)
+    auto k = conv3x3_halo_persist_kernel<T, BN, false>;
+    if constexpr (sizeof(T) == 2)
+      if (option(SELUNET_OPT_BF16_M16, 0) == 1) k = conv3x3_halo_persist_kernel<T, BN, false, true>;
+    hipLaunchKernelGGL(k, dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N,
+                       k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr);
     return;
   }
   auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
