@@ -57,6 +57,25 @@ def gather_wgs():
         K.query("selunet_set_gather_workgroups", prev[0])
 
 
+@pytest.fixture
+def kernel_option():
+    """Set library options (selunet_set_option) for one test, restored after."""
+    prev = []
+
+    def set_(variant):
+        if variant is not None:
+            prev.append((variant[0], K.set_option(*variant)))
+
+    yield set_
+    for name, v in reversed(prev):
+        K.set_option(name, v)
+
+
+# kernel-selection alternatives the bf16 persistent-kernel tests also run under: the 16x16x32 MFMA form
+# (SELUNET_OPT_BF16_M16) and single-chunk layers on the persistent kernel (SELUNET_OPT_HALO_PERSIST = 2)
+BF16_VARIANTS = [None, ("BF16_M16", 1), ("HALO_PERSIST", 2)]
+
+
 def gen(*shape, seed=0, scale=1.0):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(*shape, generator=g) * scale
@@ -690,10 +709,12 @@ def test_first_conv_wgrad_bn_fused(dt, cin, n, h, w):
     (256, 0, 512, 2, 32, 32),    # four chunks, four column tiles
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
-def test_conv3x3_bf16_persist_fwd_stats(cin0, cin1, cout, n, h, w, wgs, halo_wgs):
+@pytest.mark.parametrize("variant", BF16_VARIANTS)
+def test_conv3x3_bf16_persist_fwd_stats(cin0, cin1, cout, n, h, w, wgs, variant, halo_wgs, kernel_option):
     """bf16 multi-chunk 3x3 forward on the persistent halo kernel with the BN statistics epilogue;
-    wgs = 3 makes every workgroup walk several tiles."""
+    wgs = 3 makes every workgroup walk several tiles; variant: a kernel-selection option set for the test."""
     halo_wgs(wgs)
+    kernel_option(variant)
     x0 = _bf(gen(n, cin0, h, w, seed=60))
     x1 = _bf(gen(n, cin1, h, w, seed=61)) if cin1 else None
     s0, t0 = bn_fold(cin0, 62)
@@ -726,10 +747,12 @@ def test_conv3x3_bf16_persist_fwd_stats(cin0, cin1, cout, n, h, w, wgs, halo_wgs
                                                 (512, 256, 256, 32, 32), (64, 64, 0, 20, 40),
                                                 (128, 64, 64, 24, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
-def test_conv3x3_bf16_persist_dgrad(cin, cout, split, h, w, wgs, halo_wgs):
+@pytest.mark.parametrize("variant", BF16_VARIANTS)
+def test_conv3x3_bf16_persist_dgrad(cin, cout, split, h, w, wgs, variant, halo_wgs, kernel_option):
     """bf16 data gradient on the persistent halo kernel: plain with the producer's BN-backward sums,
     and the torch.cat split with the ConvTranspose2d bias column sums."""
     halo_wgs(wgs)
+    kernel_option(variant)
     n = 2
     wt = _bf(gen(cout, cin, 3, 3, seed=64, scale=0.05))
     dy = _bf(gen(n, cout, h, w, seed=65))
