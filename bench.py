@@ -452,7 +452,8 @@ def input_loop(args, dev, step, state, selective):
     h2d = (time.perf_counter() - t0) / 5
     return {"value": round(args.batch * args.steps / el, 2), "ms_per_step": round(1e3 * el / args.steps, 3),
             "includes": "data.BatchLoader (shuffled uint8 NHWC patches gathered into pinned memory on a prefetch "
-                        "thread, H2D copy as uint8, GPU normalise / flips / NCHW fp32) + step + SegMetrics",
+                        "thread, H2D copy as uint8 on a copy stream overlapping the previous step, GPU normalise / "
+                        "flips / NCHW fp32) + step + SegMetrics",
             "reference_fp32_h2d_ms": round(1e3 * h2d, 3),
             "reference_fp32_h2d_note": f"pageable fp32 [{args.batch},3,{args.size},{args.size}] .to(cuda) per step "
                                        f"(train.py:186), {xh.numel() * 4 / 1e6:.1f} MB; not in any timed value"}

@@ -203,6 +203,7 @@ class BatchLoader:
         self.epoch = 0
         self.dropped = 0
         self._pool = cf.ThreadPoolExecutor(max_workers=1)
+        self._copy_stream = None
 
     def set_epoch(self, epoch: int):
         self.epoch = int(epoch)
@@ -241,16 +242,40 @@ class BatchLoader:
     def __len__(self):
         return len(self._plan())
 
+    def _upload(self, item, copy_stream):
+        """Host batch -> device. On a GPU the copies run on `copy_stream` (an event marks their end), so
+        batch i+1 crosses PCIe while step i computes instead of in front of step i+1."""
+        gb, im, lb, fl = item
+        if copy_stream is None:
+            return gb, im.to(self.device), lb.to(self.device), fl.to(self.device), None
+        with torch.cuda.stream(copy_stream):
+            dev = [t.to(self.device, non_blocking=True) for t in (im, lb, fl)]
+            ev = torch.cuda.Event()
+            ev.record(copy_stream)
+        return (gb, *dev, ev)
+
     def __iter__(self):
         plan = self._plan()
-        fut = self._pool.submit(self._host, plan[0]) if plan else None
+        if not plan:
+            return
+        cs = None
+        if torch.device(self.device).type == "cuda":
+            if self._copy_stream is None:  # (one per loader: a stream per epoch costs a creation each time)
+                self._copy_stream = torch.cuda.Stream(device=self.device)
+            cs = self._copy_stream
+        fut = self._pool.submit(self._host, plan[0])
+        pending = self._upload(fut.result(), cs)
         for i in range(len(plan)):
-            gb, im, lb, fl = fut.result()
             if i + 1 < len(plan):
                 fut = self._pool.submit(self._host, plan[i + 1])
-            im = im.to(self.device, non_blocking=True)
-            lb = lb.to(self.device, non_blocking=True)
-            fl = fl.to(self.device, non_blocking=True)
+            gb, im, lb, fl, ev = pending
+            if ev is not None:  # the step's stream waits for the copies; the allocator learns the new user
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                for t in (im, lb, fl):
+                    t.record_stream(cur)
             parallel.set_global_batch(gb)
             x, t = prep_batch(im, lb, fl, self.input_type)
             yield x, t
+            if i + 1 < len(plan):  # (the consumer has enqueued step i: this upload overlaps it)
+                pending = self._upload(fut.result(), cs)
