@@ -640,6 +640,14 @@ int selunet_prep_batch_mode(const uint8_t* img, const uint8_t* lab, const uint8_
 int selunet_seg_metrics(const float* out, const float* sel, const float* target, int64_t p,
                         float t_out, float t_sel, unsigned long long* counts, void* stream);
 
+/* ---- multi-GPU overlap probe (bench/tools only, not on the training path) ------
+ * Stand-in for one bucketed RCCL all-reduce kernel on a single GPU: n_wg workgroups of 256 threads
+ * reduce-copy dst[i] += src[i] over their slices of [0, n) (n % 4 == 0, 16-B aligned), repeatedly,
+ * until `us` microseconds of GPU wall clock have passed since each workgroup started — holding
+ * n_wg CUs' worth of waves the way a ring all-reduce holds its channels. Issued on a side stream at
+ * GradBucketer's bucket points by tools/overlap_emulation.py. */
+int selunet_cu_hold(const float* src, float* dst, int64_t n, int32_t n_wg, float us, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -183,6 +183,7 @@ SIGNATURES = {
     "selunet_prep_batch_mode": (c_int32, [P, P, P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
     "selunet_seg_metrics": (c_int32, [P, P, P, c_int64, c_float, c_float, P, P]),
     "selunet_set_option": (c_int64, [c_int32, c_int64]),
+    "selunet_cu_hold": (c_int32, [P, P, c_int64, c_int32, c_float, P]),
 }
 
 _lib = None
@@ -203,22 +204,22 @@ def load(auto_build: bool = False):
         if _lib is not None:
             return _lib
         path = lib_path()
+        tree = _build.source_fingerprint()
+        own = "SELUNET_LIB" not in os.environ
+        if auto_build and own and (not os.path.exists(path) or _build.lib_stamp_fingerprint(path) != tree):
+            _build.build(verbose=False)  # missing or stale: rebuild before the library is mapped
         if not os.path.exists(path):
-            if auto_build:
-                _build.build(verbose=False)
-            else:
-                raise RuntimeError(
-                    f"{path} not found: the MI355X kernels are not built (run "
-                    "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`). "
-                    "There is no CPU fallback.")
+            raise RuntimeError(
+                f"{path} not found: the MI355X kernels are not built (run "
+                "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`). "
+                "There is no CPU fallback.")
         L = ctypes.CDLL(path)
         L.selunet_build_id.restype = ctypes.c_char_p
-        built_from = L.selunet_build_id().decode()
-        if "SELUNET_LIB" not in os.environ and built_from != _build.source_fingerprint():
+        built_fp, built_arch = _build.parse_build_id(L.selunet_build_id().decode())
+        if own and built_fp != tree:
             raise RuntimeError(
-                f"{path} was built from other sources (build id {built_from}, tree "
-                f"{_build.source_fingerprint()}): rebuild with "
-                "`python -m selectivenet_for_semantic_segmentation_binary_amd.build`")
+                f"{path} was built from other sources (build id {built_fp}, for {built_arch}; tree "
+                f"{tree}): rebuild with `python -m selectivenet_for_semantic_segmentation_binary_amd.build`")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -25,8 +25,11 @@ LIB = os.path.join(PKG, "libselunet.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "selunet.h")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SELUNET_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+# the source fingerprint covers these flags; the target arch (SELUNET_ARCH, default gfx950) is recorded
+# beside it in the build id, so a library built for another arch is reported as such, not as stale sources
+BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+              "-Wno-unused-but-set-variable"]
+FLAGS = BASE_FLAGS + [f"--offload-arch={ARCH}"]
 
 
 def _sources():
@@ -51,8 +54,28 @@ def _digest(paths, extra=()):
 
 
 def source_fingerprint() -> str:
-    """SHA-256 (first 24 hex digits) over every kernel source, header and the compiler flags."""
-    return _digest([os.path.join(CSRC, s) for s in _sources()] + _headers(), FLAGS)[:24]
+    """SHA-256 (first 24 hex digits) over every kernel source, header and the compiler flags (not the
+    target arch: see build_id)."""
+    return _digest([os.path.join(CSRC, s) for s in _sources()] + _headers(), BASE_FLAGS)[:24]
+
+
+def build_id(fp: str | None = None, arch: str | None = None) -> str:
+    """The string `selunet_build_id()` returns: '<source fingerprint> <arch>'."""
+    return f"{fp or source_fingerprint()} {arch or ARCH}"
+
+
+def parse_build_id(bid: str) -> tuple[str, str]:
+    fp, _, arch = bid.strip().partition(" ")
+    return fp, arch or "?"
+
+
+def lib_stamp_fingerprint(lib: str = None) -> str | None:
+    """Source fingerprint recorded next to a built library (its .sha stamp), or None."""
+    try:
+        with open((lib or LIB) + ".sha") as f:
+            return parse_build_id(f.read())[0]
+    except OSError:
+        return None
 
 
 def _stamp_ok(stamp, want):
@@ -80,8 +103,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
     heads = _headers()
-    fp = source_fingerprint()
-    # the build id: a one-line translation unit generated from the fingerprint
+    fp = build_id()
+    # the build id: a one-line translation unit generated from the fingerprint and the arch
     bid_src = os.path.join(BUILD, "build_id.hip")
     bid = f'extern "C" const char* selunet_build_id(void) {{ return "{fp}"; }}\n'
     if not os.path.exists(bid_src) or open(bid_src).read() != bid:

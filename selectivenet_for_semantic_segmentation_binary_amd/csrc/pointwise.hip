@@ -400,7 +400,7 @@ struct BnFinArgs {
   float *mean_o, *invstd_o, *scale_o, *shift_o;
   const float* center;  // non-NULL: s_sum / s_sq are sums of (y - center) and (y - center)^2
   // shifted first pass (selunet_bn_stats_finalize_shifted): uvar_flag_o = the unbiased variance, or -1
-  // where (mean - center)^2 > flag_ratio * (var + eps) (its one-pass variance is not exact enough: the
+  // where (mean - center)^2 > flag_ratio * var (its one-pass variance is not exact enough: the
   // adaptive centered pass re-reads those channels); center_next_o = mean (the next step's center,
   // may alias center: read before written, per channel)
   float* uvar_flag_o;
@@ -429,10 +429,10 @@ __device__ inline void bn_finalize_one(int c, double s_sum, double s_sq, const B
   }
   if (a.training && a.uvar_flag_o) {
     const double d = mean - (a.center ? (double)a.center[c] : 0.0);
-    // the one-pass variance's error is ~eps_fp32 * (var + d^2); what it feeds is 1/sqrt(var + eps_bn) and
-    // the running variance, so it is exact enough while d^2 <= ratio * (var + eps_bn) (a channel whose
-    // variance is far below eps_bn is not re-read for a mean shift the normalisation cannot see)
-    a.uvar_flag_o[c] = d * d <= (double)a.flag_ratio * (var + (double)a.eps)
+    // the one-pass variance's error is ~eps_fp32 * (var + d^2); it feeds 1/sqrt(var + eps_bn) and the
+    // running variance, which is compared raw (relative) with the reference's, so the criterion is on var
+    // alone: a near-constant channel (var far below eps_bn) with a mean shift is re-read too
+    a.uvar_flag_o[c] = d * d <= (double)a.flag_ratio * var
                            ? (float)(var * (double)a.count / (double)(a.count - 1)) : -1.0f;
   }
   // a non-finite batch mean is not carried into the next step's center (it would poison every later

@@ -124,34 +124,59 @@ def decode_patch_list(data_dir, data_list, patch_mag=200, patch_size=256, cache=
         for i, (a, b) in enumerate(pairs):
             imgs[i] = np.array(Image.open(os.path.join(root, a)).convert("RGB"))
             labs[i] = np.array(Image.open(os.path.join(root, b)).convert("L"))
+        if cache:
+            os.makedirs(cdir, exist_ok=True)
+            for path, arr in ((fi, imgs), (fl, labs)):
+                tmp = f"{path[:-4]}.tmp{os.getpid()}.npy"
+                np.save(tmp, arr)
+                os.replace(tmp, path)
     except Exception as e:
         if shared:  # the waiting ranks stop at once instead of polling until CACHE_WAIT_S
             os.makedirs(cdir, exist_ok=True)
             with open(failed, "w") as f:
-                f.write(f"rank 0 failed to decode the patch list: {e!r}\n")
+                f.write(f"rank 0 failed to decode or cache the patch list: {e!r}\n")
         raise
-    if cache:
-        os.makedirs(cdir, exist_ok=True)
-        for path, arr in ((fi, imgs), (fl, labs)):
-            tmp = f"{path[:-4]}.tmp{os.getpid()}.npy"
-            np.save(tmp, arr)
-            os.replace(tmp, path)
     return PatchSet(imgs, labs, ids)
 
 
 CACHE_WAIT_S = float(os.environ.get("SELUNET_CACHE_WAIT_S", 6 * 3600))
 
 
-def _wait_for_files(paths, limit_s, poll_s=0.5, failed=None):
+def _process_start_time() -> float:
+    """Wall-clock start of this process (psutil), or the import of this module without psutil."""
+    try:
+        import psutil
+
+        return float(psutil.Process().create_time())
+    except Exception:  # pragma: no cover - psutil is part of the image
+        return _IMPORT_TIME
+
+
+_IMPORT_TIME = __import__("time").time()
+
+
+def _wait_for_files(paths, limit_s, poll_s=0.5, failed=None, since=None):
     """Block until every path exists (they appear atomically, os.replace) or limit_s passes; raise
-    as soon as the `failed` marker (written by the rank that was to produce them) appears."""
+    as soon as the `failed` marker (written by the rank that was to produce them) appears.
+
+    Only a marker written by this launch counts: one whose mtime is before `since` (default: this
+    process's start) is left over from an earlier failed run — every process of a new launch starts
+    after the old run ended, while this launch's rank 0 can only fail after the process group's
+    rendezvous, i.e. after every rank has started — and is ignored (rank 0 deletes it when it starts
+    decoding)."""
     import time
 
+    since = _process_start_time() if since is None else since
     t0 = time.monotonic()
     while not all(os.path.exists(p) for p in paths):
         if failed is not None and os.path.exists(failed):
-            with open(failed) as f:
-                raise RuntimeError(f.read().strip())
+            try:
+                fresh = os.stat(failed).st_mtime >= since
+                msg = open(failed).read().strip() if fresh else None
+            except OSError:  # removed between the checks (rank 0 clearing a stale marker)
+                fresh = False
+            if fresh:
+                raise RuntimeError(msg)
         if time.monotonic() - t0 > limit_s:
             raise TimeoutError(f"rank 0 did not write the patch cache within {limit_s:.0f} s: {paths}")
         time.sleep(poll_s)

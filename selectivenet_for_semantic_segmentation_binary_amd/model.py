@@ -126,7 +126,9 @@ class _UNetBFunction(torch.autograd.Function):
             off += k
         # DataParallel reduce-add of the replica gradients: bucketed all-reduces issued while the
         # backward of the shallower layers still runs
-        bucketer = parallel.GradBucketer(flat, layout) if parallel.is_initialized() else None
+        emu = parallel.overlap_emulation()
+        bucketer = (parallel.GradBucketer(flat, layout, parallel.bucket_elems(), emulate=emu) if parallel.is_initialized() or emu is not None
+                    else None)
         ctx.eng.backward(ctx.ectx, P, G, list(g_heads), flat, on_grads=bucketer.ready if bucketer else None)
         ctx.release.detach()
         ctx.ectx = None

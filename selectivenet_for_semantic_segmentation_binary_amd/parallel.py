@@ -23,7 +23,7 @@ import os
 import torch
 import torch.distributed as dist
 
-_STATE = {"enabled": False, "group": None, "global_batch": None}
+_STATE = {"enabled": False, "group": None, "global_batch": None, "emulate": None, "bucket_elems": 1 << 20}
 
 
 def init_data_parallel(backend: str | None = None, group=None) -> tuple[int, int]:
@@ -56,6 +56,71 @@ def global_batch() -> int | None:
 
 def is_initialized() -> bool:
     return _STATE["enabled"] and dist.is_initialized()
+
+
+class OverlapEmulation:
+    """One-GPU stand-in for the bucketed gradient all-reduce (tools/overlap_emulation.py).
+
+    At each point GradBucketer would issue an RCCL all-reduce, a CU-holding reduce-copy kernel
+    (`selunet_cu_hold`: n_wg workgroups, `us` microseconds of wall clock each) is launched on a side
+    stream that first waits on the compute stream — the stream relationship ProcessGroupNCCL sets
+    up — and `finish` makes the compute stream wait for it, as `Work.wait()` does. The kernel reads
+    the bucket and reduce-copies into a scratch buffer, so the gradients are untouched. `events`
+    collects (bucket elements, start, end) HIP event pairs on the side stream when timing is on."""
+
+    def __init__(self, n_wg: int, us: float, timing: bool = False, model: tuple | None = None):
+        # model (alpha_us, beta_GBs): hold each bucket's CUs for alpha + bytes / beta instead of `us`
+        self.n_wg, self.us, self.timing, self.model = int(n_wg), float(us), timing, model
+        self.held_us = 0.0
+        self.side = None
+        self.scratch = None
+        self.events = []
+
+    def launch(self, t: torch.Tensor):
+        from . import _lib as K
+        if self.side is None:
+            self.side = torch.cuda.Stream(device=t.device)
+        if self.scratch is None or self.scratch.numel() < t.numel() + 4:
+            self.scratch = torch.zeros(t.numel() + 4, dtype=torch.float32, device=t.device)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        self.side.wait_event(ev)
+        n = (t.numel() // 4) * 4
+        us = self.us if self.model is None else self.model[0] + t.numel() * 4 / (self.model[1] * 1e3)
+        self.held_us += us
+        with torch.cuda.stream(self.side):
+            e0 = e1 = None
+            if self.timing:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.side)
+            K.call("selunet_cu_hold", K.ptr(t), K.ptr(self.scratch), max(n, 4), self.n_wg, us,
+                   self.side.cuda_stream)
+            if self.timing:
+                e1.record(self.side)
+                self.events.append((t.numel(), e0, e1))
+
+    def finish(self, device):
+        if self.side is not None:
+            torch.cuda.current_stream(device).wait_stream(self.side)
+
+
+def set_overlap_emulation(emu: "OverlapEmulation | None"):
+    """Install (or remove, None) the one-GPU all-reduce stand-in: with it, the backward builds a
+    GradBucketer on a single process and launches the stand-in kernel at every bucket point."""
+    _STATE["emulate"] = emu
+
+
+def overlap_emulation() -> "OverlapEmulation | None":
+    return _STATE["emulate"]
+
+
+def set_bucket_elems(n: int):
+    """Minimum gradient-bucket size in floats (default 1 << 20 = 4 MB)."""
+    _STATE["bucket_elems"] = int(n)
+
+
+def bucket_elems() -> int:
+    return _STATE["bucket_elems"]
 
 
 def world_size() -> int:
@@ -105,9 +170,10 @@ class GradBucketer:
     anything left and makes the current stream wait for all of them. Every rank reports the layers
     in the same order, so the collectives are issued in the same order everywhere."""
 
-    def __init__(self, flat: torch.Tensor, layout, bucket_elems: int = 1 << 20):
+    def __init__(self, flat: torch.Tensor, layout, bucket_elems: int = 1 << 20, emulate: OverlapEmulation = None):
         # layout: [(param_name, offset, numel)] in flat order
         self.flat = flat
+        self.emulate = emulate
         self.buckets = []          # [lo, hi, pending layer set]
         self.works = []
         cur_hi, cur_lo, layers = None, None, set()
@@ -129,6 +195,8 @@ class GradBucketer:
         if is_initialized():
             self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_STATE["group"],
                                               async_op=True))
+        elif self.emulate is not None:
+            self.emulate.launch(self.flat[lo:hi])
 
     def ready(self, layer: str):
         for i, b in enumerate(self.buckets):
@@ -144,6 +212,8 @@ class GradBucketer:
         for w in self.works:
             w.wait()
         self.works = []
+        if self.emulate is not None:
+            self.emulate.finish(self.flat.device)
         return self.flat
 
 

@@ -127,3 +127,18 @@ def test_product_path_has_no_cpu_fallback():
         net(torch.zeros(1, 3, 16, 16))
     with pytest.raises(RuntimeError):
         S.calc_selective_risk_image_b(torch.zeros(1, 4, 4), torch.zeros(1, 4, 4), torch.zeros(1, 4, 4))
+
+
+def test_build_id_carries_the_sources_and_the_arch(lib, tmp_path):
+    """the library's build id is '<source fingerprint> <arch>'; the fingerprint leaves the
+    target arch out (a library built for another SELUNET_ARCH is reported as such), and the .sha stamp
+    next to the library is what load(auto_build=True) compares before mapping it (stale -> rebuild)."""
+    lib.selunet_build_id.restype = ctypes.c_char_p
+    fp, arch = B.parse_build_id(lib.selunet_build_id().decode())
+    assert fp == B.source_fingerprint() and arch == B.ARCH
+    assert B.lib_stamp_fingerprint(K.lib_path()) == fp
+    stamp = tmp_path / "x.so.sha"
+    stamp.write_text("0123abcd gfx942")
+    assert B.lib_stamp_fingerprint(str(tmp_path / "x.so")) == "0123abcd"
+    assert B.lib_stamp_fingerprint(str(tmp_path / "missing.so")) is None
+    assert not any("offload-arch" in f for f in B.BASE_FLAGS)

@@ -159,6 +159,58 @@ def test_decode_patch_list_cache_is_written_atomically(tmp_path):
     assert np.array_equal(np.asarray(b.labels), a.labels)
 
 
+def test_cache_wait_ignores_a_stale_failure_marker(tmp_path):
+    """a {key}_FAILED marker left by an earlier failed run (mtime before this process
+    started) must not stop a waiting rank — it keeps polling and picks up the cache rank 0 writes —
+    while a marker written during this launch still stops it at once."""
+    import threading
+    import time
+
+    files = [str(tmp_path / "a.npy"), str(tmp_path / "b.npy")]
+    failed = tmp_path / "k_FAILED"
+    failed.write_text("rank 0 failed to decode the patch list: old error\n")
+    old = time.time() - 3600
+    os.utime(failed, (old, old))
+
+    def produce():
+        time.sleep(0.3)
+        for f in files:
+            np.save(f, np.zeros(1))
+
+    th = threading.Thread(target=produce)
+    th.start()
+    D._wait_for_files(files, 30, poll_s=0.05, failed=str(failed))  # returns: the marker is stale
+    th.join()
+    for f in files:
+        os.remove(f)
+    failed.write_text("rank 0 failed to decode the patch list: new error\n")  # fresh: this launch's
+    with pytest.raises(RuntimeError, match="new error"):
+        D._wait_for_files(files, 30, poll_s=0.05, failed=str(failed))
+
+
+def test_cache_write_failure_leaves_the_marker(tmp_path, monkeypatch):
+    """a failure while writing the cache (np.save / os.replace) writes the failure marker
+    too, so waiting ranks stop instead of polling for CACHE_WAIT_S."""
+    from PIL import Image
+
+    root = tmp_path / "200x_16"
+    root.mkdir()
+    Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(root / "p0_input.png")
+    Image.fromarray(np.zeros((16, 16), np.uint8)).save(root / "p0_label.png")
+    monkeypatch.setattr(D.parallel, "is_initialized", lambda: True)
+    monkeypatch.setattr(D.parallel, "world_size", lambda: 2)
+    monkeypatch.setattr(D.parallel, "rank", lambda: 0)
+
+    def boom(*a, **k):
+        raise OSError("disk full")
+
+    monkeypatch.setattr(D.np, "save", boom)
+    with pytest.raises(OSError, match="disk full"):
+        D.decode_patch_list(str(tmp_path), [("p0_input.png", "p0_label.png")], 200, 16)
+    markers = [f for f in os.listdir(root / "_selunet_cache") if f.endswith("_FAILED")]
+    assert len(markers) == 1 and "disk full" in (root / "_selunet_cache" / markers[0]).read_text()
+
+
 def test_spawn_reports_the_failing_rank_not_the_terminated_siblings():
     """train.spawn (one process per --local_rank id): rank 1 fails with code 3 while rank 0 would run
     for minutes; spawn stops rank 0 and returns 3 (not rank 0's -SIGTERM)."""

@@ -55,12 +55,16 @@ def run(xtr, ltr, xva, lva, a, member):
             tr.add_batch(o.detach(), lab, s.detach())
     net.eval()
     vp = SegMetrics(dev, selective=False, rule="train")
+    vs = SegMetrics(dev, selective=True, rule="train")
     xv, lv = torch.tensor(xva, device=dev), torch.tensor(lva, device=dev)
     with torch.no_grad():
         for b0 in range(0, xv.shape[0], a.bs):
             o, s, _ = net(xv[b0:b0 + a.bs])
             vp.add_batch(o, lv[b0:b0 + a.bs], s)
-    return mean_iou(tr.confusion_matrix()), mean_iou(vp.confusion_matrix()), float(loss.item())
+            vs.add_batch(o, lv[b0:b0 + a.bs], s)
+    cms = vs.confusion_matrix()
+    return (mean_iou(tr.confusion_matrix()), mean_iou(vp.confusion_matrix()), float(loss.item()), mean_iou(cms),
+            float(np.asarray(cms).sum()) / lva.size, float(np.asarray(cms)[1].sum()) / max(1.0, float(lva.sum())))
 
 
 def main():
@@ -77,13 +81,15 @@ def main():
     ap.add_argument("--lr-min", type=float, default=1e-5)
     ap.add_argument("-k", type=int, default=8)
     ap.add_argument("--hard", default="", help="';'-separated make_patches_hard settings "
-                    "'contrast,noise,texture,decoys' to sweep (empty: make_patches)")
+                    "'contrast,noise,texture,decoys[,tumorable_frac]' to sweep (empty: make_patches)")
     a = ap.parse_args()
     for cfg in (a.hard.split(";") if a.hard else [None]):
         if cfg:
-            c, nz, tx, dc = (float(v) for v in cfg.split(","))
+            vals = [float(v) for v in cfg.split(",")]
+            c, nz, tx, dc = vals[:4]
+            tf = vals[4] if len(vals) > 4 else 0.39
             gen = lambda n, seed: make_patches_hard(n, a.size, seed=seed, contrast=c, noise=nz, texture=tx,  # noqa
-                                                    decoys=int(dc))
+                                                    decoys=int(dc), tumorable_frac=tf)
         else:
             gen = lambda n, seed: make_patches(n, a.size, seed=seed)  # noqa: E731
         xtr, ltr = preprocess(*gen(a.n_train, 2024))
@@ -91,10 +97,14 @@ def main():
         res = [run(xtr, ltr, xva, lva, a, m) for m in range(a.k + 1)]
         tr = np.array([r[0] for r in res])
         va = np.array([r[1] for r in res])
+        vs = np.array([r[3] for r in res])
         print(f"cfg {vars(a)} hard={cfg}")
+        print("val selective mIoU", np.round(vs, 5), "coverage", [round(r[4], 4) for r in res],
+              "tumour pixels kept", [round(r[5], 4) for r in res], "tumour fraction", round(float(lva.mean()), 4))
         print("train mIoU", np.round(tr, 5), "val mIoU", np.round(va, 5), "final loss", [round(r[2], 4) for r in res])
         print(f"SPREAD hard={cfg} train {np.abs(tr[1:] - tr[0]).max():.5f} val {np.abs(va[1:] - va[0]).max():.5f} "
-              f"val range {va.max() - va.min():.5f} val0 {va[0]:.5f}", flush=True)
+              f"val range {va.max() - va.min():.5f} val0 {va[0]:.5f} | selective spread "
+              f"{np.abs(vs[1:] - vs[0]).max() if len(vs) > 1 else 0:.5f} sel0 {vs[0]:.5f}", flush=True)
 
 
 if __name__ == "__main__":
