@@ -60,6 +60,9 @@ enum {
                                    * 1 every eligible layer, 2 inputs of at most 64 channels, 3 (default) those of
                                    * them whose source carries a BN+ReLU transform (the forwards) */
   SELUNET_OPT_BF16_M16,           /* bf16 persistent 3x3 kernel on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0) */
+  SELUNET_OPT_TILE_QUEUE,         /* split-fp16 persistent 3x3 kernel: pixel tiles from a ticket counter, statistics
+                                   * per tile (1), or the static walk (0, default); selunet_conv3x3_x2_stats_rows
+                                   * follows it (robustness to a concurrent all-reduce) */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
@@ -213,6 +216,18 @@ int64_t selunet_conv3x3_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet
 int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
                              float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
                              void* stream);
+/* selunet_conv3x3_wgrad_x2 with the layer's BN-backward apply fused into its dY staging (replaces
+ * selunet_bn_bwd_apply_amax + selunet_conv3x3_wgrad_x2; model.py:12-13's backward): p gathers dA (one
+ * source, no transform), bnb the forward's y / scale / shift / mean / invstd (slab unused), coef the
+ * [3][C] coefficients of selunet_bn_bwd_stats_finalize; the kernel forms
+ * dy = (y*scale+shift > 0 ? k0*dA : 0) - k1 - k2*invstd*(y - mean) exactly as selunet_bn_bwd_apply,
+ * stages it split-fp16 with the range word amax_p (an upper bound of |dy|:
+ * selunet_bn_bwd_stats_finalize_bound), and writes dy [M][C] (fp32, nullable) with its exact max |dy|
+ * into *dy_amax (atomic max; zeroed by the caller) for the layer's data gradient. */
+int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                                const selunet_bn_bwd_stats* bnb, const float* coef, float* dy, float* dy_amax,
+                                void* stream);
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, int32_t n_cols, int32_t mode, int32_t split);
@@ -418,6 +433,14 @@ int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, d
                                   int64_t count, int32_t c, const float* gamma, const float* invstd,
                                   float* dgamma, float* dbeta, float* dbias, float* coef,
                                   void* stream);
+/* selunet_bn_bwd_stats_finalize that also folds an upper bound of |dy| into *bound (zeroed by the
+ * caller; atomic max over the channels of 1.25 * (|k0| amax_da + |k1| + |k2| sqrt(count)), amax_da the
+ * exact max |dA| its producer recorded): the range word selunet_conv3x3_wgrad_x2_bn stages dy with
+ * before dy exists. */
+int selunet_bn_bwd_stats_finalize_bound(const float* slab, int64_t rows, double* ws, double* sums,
+                                        int64_t count, int32_t c, const float* gamma, const float* invstd,
+                                        float* dgamma, float* dbeta, float* dbias, float* coef,
+                                        const float* amax_da, float* bound, void* stream);
 /* dy = coef0*dA - coef1 - coef2*xhat (the conv-output gradient). */
 int selunet_bn_bwd_apply(const void* dz, const void* y, int64_t m, int32_t c, const float* scale,
                          const float* shift, const float* mean, const float* invstd,

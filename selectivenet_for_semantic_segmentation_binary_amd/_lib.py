@@ -104,6 +104,8 @@ SIGNATURES = {
                                         P, P, P]),
     "selunet_conv3x3_wgrad_x2": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int64, P, P, P, P,
                                            P]),
+    "selunet_conv3x3_wgrad_x2_bn": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int64, P, P, P, P,
+                                              ctypes.POINTER(BnBwdStats), P, P, P, P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_gemm_gather_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),
@@ -128,6 +130,7 @@ SIGNATURES = {
     "selunet_bn_stats_finalize_centered_bound": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P,
                                                            c_float, c_float, P, P, P, P, P, P]),
     "selunet_bn_bwd_stats_finalize": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P]),
+    "selunet_bn_bwd_stats_finalize_bound": (c_int32, [P, c_int64, P, P, c_int64, c_int32, P, P, P, P, P, P, P, P, P]),
     "selunet_bn_bwd_apply": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_amax": (c_int32, [P, P, c_int64, c_int32, P, P, P, P, P, P, P, c_int32, P]),
     "selunet_bn_bwd_apply_heads": (c_int32, [P, c_int64, P, P, P, P, P, P, c_int32, P, P, P, P, P, c_int32, P]),
@@ -238,7 +241,7 @@ def load(auto_build: bool = False):
 OPT = {name: i for i, name in enumerate([
     "HALO", "HALO_PERSIST", "WINO", "WINO_WGRAD", "WINO_WGRAD_TW", "WINO_WGRAD_WAVES", "WGRAD_WGS",
     "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "WX2", "X2D",
-    "BF16_M16"])}
+    "BF16_M16", "TILE_QUEUE"])}
 # environment variables the host maps onto options at load (A/B and ablation runs of tools/ and the
 # exact-fp32 comparison paths of the tests); SELUNET_NO_HALO=1 means HALO=0
 ENV_OPTIONS = {f"SELUNET_{k}": v for k, v in OPT.items() if k != "HALO"}

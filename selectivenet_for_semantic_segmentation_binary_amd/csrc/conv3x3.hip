@@ -297,11 +297,21 @@ conv3x3_halo_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiA
 // A wave's 16x16 subtiles: one tile row (16 px) x 16 columns; one MFMA covers a tap's whole
 // 32-channel chunk (lane: row/column lane & 15, channels 8 (lane >> 4) .. + 7); weight rows are 160 B
 // so the 16 rows of a ds_read_b128 lane group hit distinct bank slots.
-template <typename T, int BN, bool X2, bool M16 = false>
+// TQ (split-fp16 only, SELUNET_OPT_TILE_QUEUE): the workgroups of a column tile take their pixel tiles from an
+// atomic ticket counter instead of the static walk prow, prow + gp, ..., so a launch whose workgroups cannot
+// all start at once (CUs held by a concurrent RCCL all-reduce kernel) rebalances instead of
+// ending with its late workgroups' whole share. The next tile is claimed one tile ahead (tap 0 of chunk 0,
+// consumed at chunk 1), so the atomic's latency hides under the MFMAs. The statistics (BN sums, BN-backward
+// sums, column sums) are flushed per tile into slab row = tile index — results are independent of which
+// workgroup ran a tile, so the launch stays deterministic. tq: [2][n_tiles] counters (tickets, finished
+// workgroups), zero between launches: the last workgroup of a column tile to finish resets both.
+template <typename T, int BN, bool X2, bool M16 = false, bool TQ = false>
 __global__ void __launch_bounds__(HTHREADS, 1)
 conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_pad, EpiArg ep, int n_tiles,
                             int tiles_x, int tiles_y, int ptiles, int gp, const float* __restrict__ wcs,
-                            const float* __restrict__ amax0, const float* __restrict__ amax1) {
+                            const float* __restrict__ amax0, const float* __restrict__ amax1,
+                            unsigned* __restrict__ tq = nullptr) {
+  static_assert(!TQ || X2, "tile queue: split-fp16 kernel only");
   static_assert(!X2 || std::is_same<T, float>::value, "split-fp16 form of fp32 operands only");
   static_assert(!M16 || X2 || std::is_same<T, __bf16>::value, "16x16x32 form: split-fp16 or bf16");
   constexpr int E = 16 / sizeof(T);
@@ -341,8 +351,16 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   const int n_tile = lb % n_tiles;
   const int prow = lb / n_tiles;
   const int n0 = n_tile * BN;
-  const int ntl = prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0;  // host: gp <= ptiles, so >= 1
   const int nchunks = g.Ctot / CK;
+  const int ntl = TQ ? 0 : (prow < ptiles ? (ptiles - prow + gp - 1) / gp : 0);  // host: gp <= ptiles, so >= 1
+  // TQ: this workgroup's tiles are claimed tickets (>= ptiles: none left); static: prow, prow + gp, ...
+  __shared__ int tq_slot;
+  int pt_cur = 0, pt_next = 0;
+  if constexpr (TQ) {
+    if (tid == 0) tq_slot = (int)min(atomicAdd(tq + n_tile, 1u), (unsigned)ptiles);
+    __syncthreads();
+    pt_cur = tq_slot;
+  }
   const int csteps = nchunks * 9;  // steps per tile
   float xs = 1.0f;       // X2: operand scale 2^e
   float cfac[AN] = {};   // X2: accumulator unscale per column subtile (this lane's column)
@@ -377,8 +395,8 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     }
   };
 
-  auto tile_xy = [&](int i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
-    const unsigned pt = (unsigned)(prow + i * gp);
+  auto tile_xy = [&](int pt_i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
+    const unsigned pt = (unsigned)pt_i;
     const unsigned r = pt / (unsigned)tiles_x;
     x0 = (int)(pt - r * (unsigned)tiles_x) * TW;
     const unsigned r2 = r / (unsigned)tiles_y;
@@ -549,9 +567,9 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   };
 
   // ---------------------------------------------------------------- prologue: tile 0 chunk 0, B(0), B(1)
-  {
+  if (!TQ || pt_cur < ptiles) {
     int img, y0, x0;
-    tile_xy(0, img, y0, x0);
+    tile_xy(TQ ? pt_cur : prow, img, y0, x0);
     int c0;
     const SrcArg sa = chunk_src(0, c0);
     uint4 v0[A_ROUNDS];
@@ -574,21 +592,25 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
   static_assert(stats_flush_bytes<BN, HTHREADS, Acc>() <= (int)sizeof(smem), "statistics scratch exceeds LDS");
   Acc s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float amx = 0.0f;  // running max |stored value| (epilogue range word)
-  const TileStats ts = tile_stats(ep, prow, n0, N);
+  const TileStats ts = tile_stats(ep, TQ ? 0 : prow, n0, N);
   float* tile = reinterpret_cast<float*>(smem);  // epilogue: [256][BN + 4] over the whole LDS
   uint4 ra[A_ROUNDS];
   int J = 0;  // job (tile, chunk) counter: halo buffer J & 1
   int S = 0;  // step counter: weight buffer S & 1
-  for (int i = 0; i < ntl; ++i) {
+  unsigned claimed = 0;  // TQ: the ticket tid 0 claims during a tile
+  for (int i = 0; TQ ? pt_cur < ptiles : i < ntl; ++i) {
     int img, y0, x0;
-    tile_xy(i, img, y0, x0);
+    tile_xy(TQ ? pt_cur : prow + i * gp, img, y0, x0);
     BRegs rb_hold;
     for (int c = 0; c < nchunks; ++c, ++J) {
+      if constexpr (TQ) {
+        if (c == 1) pt_next = tq_slot;  // the ticket claimed at chunk 0 (nchunks >= 2)
+      }
       const bool last_c = c + 1 == nchunks;
-      const bool has_next = !last_c || i + 1 < ntl;
+      const bool has_next = !last_c || (TQ ? pt_next < ptiles : i + 1 < ntl);
       const bool defer = last_c && has_next;  // next job is the next tile: LDS writes after the epilogue
       int nimg = img, ny0 = y0, nx0 = x0;
-      if (defer) tile_xy(i + 1, nimg, ny0, nx0);
+      if (defer) tile_xy(TQ ? pt_next : prow + (i + 1) * gp, nimg, ny0, nx0);
       const int nc = !has_next ? c : (last_c ? 0 : c + 1);
       int cs;
       const SrcArg sn = chunk_src(nc, cs);
@@ -608,7 +630,13 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
             ra[r] = *a_ptr(sn, cs, nimg, ny0, nx0, hp, cc);
           }
         }
+        if constexpr (TQ) {
+          if (c == 0 && t == 0 && tid == 0) claimed = atomicAdd(tq + n_tile, 1u);  // the next tile's ticket
+        }
         mma_step(J & 1, S & 1, t);
+        if constexpr (TQ) {
+          if (c == 0 && t == 8 && tid == 0) tq_slot = (int)min(claimed, (unsigned)ptiles);  // read at chunk 1
+        }
         if (defer && t == 8) rb_hold = rb_next;  // B(S + 1): stored after the epilogue
         else b_store(rb_next, (S + 1) & 1);
         if (!defer) {
@@ -681,11 +709,21 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       return reinterpret_cast<T*>(ep.out0) + m * N + col;
     };
     auto bias_col = [&](int cl) { return n0 + cl; };
-    lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
-    if (i + 1 < ntl) {
+    if constexpr (TQ) {
+      // this tile's statistics go to slab row pt_cur (the range word stays per workgroup: one atomic at the end)
+      TileStats tt = tile_stats(ep, pt_cur, n0, N);
+      tt.amax = nullptr;
+      lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, tt, s1, s2, s3, amx);
+      tile_stats_flush<BN, HTHREADS>(tile, tid, tt, s1, s2, s3, 0.0f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s1[e] = s2[e] = s3[e] = 0;
+    } else {
+      lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, ts, s1, s2, s3, amx);
+    }
+    if (TQ ? pt_next < ptiles : i + 1 < ntl) {
       __syncthreads();  // the tile has been read: LDS back to halo / weights
       int nimg, ny0, nx0;
-      tile_xy(i + 1, nimg, ny0, nx0);
+      tile_xy(TQ ? pt_next : prow + (i + 1) * gp, nimg, ny0, nx0);
       int cs;
       const SrcArg sn = chunk_src(0, cs);
 #pragma unroll
@@ -693,8 +731,18 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       b_store(rb_hold, S & 1);
       __syncthreads();
     }
+    if constexpr (TQ) pt_cur = pt_next;
   }
-  tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
+  if constexpr (TQ) {
+    if (ts.amax) block_amax(ts.amax, amx, tile);
+    if (tid == 0 && atomicAdd(tq + n_tiles + n_tile, 1u) == (unsigned)gp - 1u) {
+      // every workgroup of this column tile has made its last claim: reset for the next launch
+      atomicExch(tq + n_tile, 0u);
+      atomicExch(tq + n_tiles + n_tile, 0u);
+    }
+  } else {
+    tile_stats_flush<BN, HTHREADS>(tile, tid, ts, s1, s2, s3, amx);
+  }
 }
 
 // =========================================================================== fp32 Winograd F(2,3)
@@ -1254,23 +1302,29 @@ conv3x3_wgrad_halo_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int
 // (one source per 64-channel chunk, so one scale per workgroup) and reduced like the halo kernels'.
 constexpr int XTH = 8, XTW = 8, XHW = XTW + 2, XHP = (XTH + 2) * XHW, XPIX = XTH * XTW;
 
-template <int BI>
+// The BN-backward apply fused into the weight gradient's dY staging (selunet_conv3x3_wgrad_x2_bn): P gathers
+// the layer's dA; y, the forward's folded scale / shift (ReLU mask), mean / invstd and the coefficients coef
+// [3][C] of selunet_bn_bwd_stats_finalize form dy = (y sc + sh > 0 ? k0 dA : 0) - k1 - k2 invstd (y - mean)
+// exactly as bn_bwd_apply_kernel; the workgroups of channel chunk 0 write dy (once per element) and the
+// exact max |dy| (atomic max) for the layer's data gradient (WgradBnArg, gemm_common.h).
+template <int BI, bool BNA = false>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_chunks, int64_t tiles_per_split,
                         int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
                         const float* __restrict__ amax_p, const float* __restrict__ amax_q0,
-                        const float* __restrict__ amax_q1) {
+                        const float* __restrict__ amax_q1, WgradBnArg bn) {
   constexpr int LDP = BI + 32;                   // dY plane row stride (halves): 16 dwords mod 64
   constexpr int LDX = 64 + 32;                   // halo plane row stride (halves)
   constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
   constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
   constexpr int P_ROUNDS = (XPIX * BI / 4) / 512;
   constexpr int X_ROUNDS = (XHP * 16 + 511) / 512;
+  constexpr int KX = BNA ? 5 * BI : 2 * BI;      // coefficient area: dY side (sc, sh[, k0, a, b]), then the halo's
   static_assert(P_ROUNDS * 512 == XPIX * BI / 4, "dY tile must split evenly over the threads");
 
   __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][XPIX][LDP];  // [buffer][h, l][pixel][co]
   __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][XHP][LDX];   // [buffer][h, l][halo pixel][ci]
-  __shared__ float Ks[2 * BI + 2 * 64];
+  __shared__ float Ks[KX + 2 * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1304,7 +1358,24 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   const float sp = x2_scale(amax_p[0], &uns_p);
   const float sx = x2_scale((xs_src ? amax_q1 : amax_q0)[0], &uns_x);
 
-  if (tid < 2 * BI + 128) {
+  if constexpr (BNA) {
+    for (int k = tid; k < KX; k += 512) {
+      const int c = i0 + (k % BI), C = P.Ctot;
+      float v;
+      switch (k / BI) {
+        case 0: v = bn.scale[c]; break;
+        case 1: v = bn.shift[c]; break;
+        case 2: v = bn.coef[c]; break;                                       // k0
+        case 3: v = bn.coef[2 * C + c] * bn.invstd[c]; break;                // a = k2 invstd
+        default: v = bn.coef[C + c] - bn.coef[2 * C + c] * bn.invstd[c] * bn.mean[c];  // b = k1 - a mean
+      }
+      Ks[k] = v;
+    }
+    if (tid < 128) {
+      const int c = xc + (tid % 64);
+      Ks[KX + tid] = xa.scale ? (tid < 64 ? xa.scale[c] : xa.shift[c]) : 0.0f;
+    }
+  } else if (tid < 2 * BI + 128) {
     float v;
     if (tid < 2 * BI) {
       const int c = i0 + (tid % BI);
@@ -1315,6 +1386,8 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
     }
     Ks[tid] = v;
   }
+  float dam = 0.0f;                               // BNA: running max |dy| of this workgroup's stores
+  const bool dy_out = BNA && cik == 0 && bn.dy != nullptr;
 
   auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
     const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
@@ -1344,16 +1417,21 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
     *reinterpret_cast<f16x4*>(lp) = l;
   };
   float4 rp[P_ROUNDS], rx[X_ROUNDS];
-  auto load_p = [&](int pt) __attribute__((always_inline)) {
+  float4 ry[BNA ? P_ROUNDS : 1];                  // BNA: y at the dA elements
+  // rounds [r0, r1) of the dY tile (BNA at BI = 128 stages it in two halves: dA and y of half a tile live
+  // at a time, as many registers as the plain kernel's whole dY tile)
+  auto load_p = [&](int pt, int r0, int r1) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
+      if (r < r0 || r >= r1) continue;
       const int idx = r * 512 + tid;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const int y = min(y0 + px / XTW, H - 1), x = min(x0 + px % XTW, W - 1);
-      rp[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pa.data) +
-                                               (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4);
+      const int64_t off = (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4;
+      rp[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pa.data) + off);
+      if constexpr (BNA) ry[r] = *reinterpret_cast<const float4*>(bn.y + off);
     }
   };
   auto load_x = [&](int pt) __attribute__((always_inline)) {
@@ -1368,16 +1446,36 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
                                                (((int64_t)img * H + y) * W + x) * xa.C + xc + cc * 4);
     }
   };
-  auto store_p = [&](int pt, int buf) __attribute__((always_inline)) {
+  auto store_p = [&](int pt, int buf, int r0, int r1) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
+      if (r < r0 || r >= r1) continue;
       const int idx = r * 512 + tid;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const bool in = y0 + px / XTW < H && x0 + px % XTW < W;
-      put(in ? rp[r] : make_float4(0, 0, 0, 0), pa.scale && in ? Ks + cc * 4 : nullptr, Ks + BI + cc * 4, pa.relu,
-          sp, &Ps[buf][0][px][cc * 4], &Ps[buf][1][px][cc * 4]);
+      if constexpr (BNA) {
+        // dy of 4 channels (bn_bwd_apply_kernel's arithmetic), written once by channel chunk 0
+        const float g[4] = {rp[r].x, rp[r].y, rp[r].z, rp[r].w}, yv[4] = {ry[r].x, ry[r].y, ry[r].z, ry[r].w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = cc * 4 + e;
+          o[e] = (yv[e] * Ks[c] + Ks[BI + c] > 0.0f ? Ks[2 * BI + c] * g[e] : 0.0f) - Ks[4 * BI + c] -
+                 Ks[3 * BI + c] * yv[e];
+        }
+        const float4 d = in ? make_float4(o[0], o[1], o[2], o[3]) : make_float4(0, 0, 0, 0);
+        if (dy_out && in) {
+          const int64_t off = (((int64_t)img * H + y0 + px / XTW) * W + x0 + px % XTW) * pa.C + i0 + cc * 4;
+          *reinterpret_cast<float4*>(bn.dy + off) = d;
+          dam = fmaxf(dam, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
+        }
+        put(d, nullptr, nullptr, 0, sp, &Ps[buf][0][px][cc * 4], &Ps[buf][1][px][cc * 4]);
+      } else {
+        put(in ? rp[r] : make_float4(0, 0, 0, 0), pa.scale && in ? Ks + cc * 4 : nullptr, Ks + BI + cc * 4, pa.relu,
+            sp, &Ps[buf][0][px][cc * 4], &Ps[buf][1][px][cc * 4]);
+      }
     }
   };
   auto store_x = [&](int pt, int buf) __attribute__((always_inline)) {
@@ -1390,8 +1488,8 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
         const int hp = idx >> 4, cc = idx & 15;
         const int y = y0 - 1 + hp / XHW, x = x0 - 1 + hp % XHW;
         const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-        put(in ? rx[r] : make_float4(0, 0, 0, 0), xa.scale && in ? Ks + 2 * BI + cc * 4 : nullptr,
-            Ks + 2 * BI + 64 + cc * 4, xa.relu, sx, &Xs[buf][0][hp][cc * 4], &Xs[buf][1][hp][cc * 4]);
+        put(in ? rx[r] : make_float4(0, 0, 0, 0), xa.scale && in ? Ks + KX + cc * 4 : nullptr,
+            Ks + KX + 64 + cc * 4, xa.relu, sx, &Xs[buf][0][hp][cc * 4], &Xs[buf][1][hp][cc * 4]);
       }
     }
   };
@@ -1401,10 +1499,10 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
 
   if (pt_begin < pt_end) {
-    load_p((int)pt_begin);
+    load_p((int)pt_begin, 0, P_ROUNDS);
     load_x((int)pt_begin);
     __syncthreads();  // coefficients visible
-    store_p((int)pt_begin, 0);
+    store_p((int)pt_begin, 0, 0, P_ROUNDS);
     store_x((int)pt_begin, 0);
     __syncthreads();
   }
@@ -1420,13 +1518,21 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
     for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
       const bool more = pt + 1 < (int)pt_end;
       // the next tile goes to the free buffer in two halves (dY after k-step 1, the halo at the end),
-      // so only one half's staging registers are live at a time
-      load_p(more ? pt + 1 : pt);
+      // so only one half's staging registers are live at a time (BNA at BI = 128: dA and y in two
+      // quarters, after k-steps 0 and 1)
+      constexpr bool QSPLIT = BNA && BI == 128;
+      constexpr int PH = QSPLIT ? P_ROUNDS / 2 : P_ROUNDS;
+      load_p(more ? pt + 1 : pt, 0, PH);
       __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
 #pragma unroll
       for (int ks = 0; ks < XPIX / 16; ++ks) {  // two tile rows (16 pixels) per k-step
+        if (QSPLIT && ks == 1) {
+          if (more) store_p(pt + 1, buf ^ 1, 0, PH);
+          load_p(more ? pt + 1 : pt, PH, P_ROUNDS);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if (ks == 2) {
-          if (more) store_p(pt + 1, buf ^ 1);
+          if (more) store_p(pt + 1, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
           load_x(more ? pt + 1 : pt);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1475,6 +1581,10 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   else if (tg == 0) tile_loop(std::integral_constant<int, 5>{});
   else tile_loop(std::integral_constant<int, 4>{});
 
+  if constexpr (BNA) {
+    // the exact max |dy| of the stored dy: one atomic per workgroup of channel chunk 0 (uniform branch)
+    if (cik == 0 && bn.dy_amax) block_amax(bn.dy_amax, dam, Ks);
+  }
   const float ofac = uns_p * uns_x;
   const int ctot = Q.Ctot;
 #pragma unroll
@@ -2026,7 +2136,7 @@ int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t*
 }
 
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
-                            const float* amax_q0, const float* amax_q1, hipStream_t st) {
+                            const float* amax_q0, const float* amax_q1, hipStream_t st, const WgradBnArg* bn) {
   const int bi = p.K % 128 == 0 ? 128 : 64;
   const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
   const int tiles_x = (int)cdiv(q.w, XTW), tiles_y = (int)cdiv(q.h, XTH);
@@ -2034,9 +2144,10 @@ int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, i
   int64_t per;
   const int64_t splits = conv3x3_wgrad_x2_splits(p, q, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
-  auto k = bi == 128 ? conv3x3_wgrad_x2_kernel<128> : conv3x3_wgrad_x2_kernel<64>;
+  auto k = bi == 128 ? (bn ? conv3x3_wgrad_x2_kernel<128, true> : conv3x3_wgrad_x2_kernel<128, false>)
+                     : (bn ? conv3x3_wgrad_x2_kernel<64, true> : conv3x3_wgrad_x2_kernel<64, false>);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(512), 0, st, p, q, ldo, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
-                     ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1);
+                     ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1, bn ? *bn : WgradBnArg{});
   return check_launch("conv3x3_wgrad_x2");
 }
 
@@ -2163,7 +2274,8 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
     if constexpr (sizeof(T) == 2)
       if (option(SELUNET_OPT_BF16_M16, 0) == 1) k = conv3x3_halo_persist_kernel<T, BN, false, true>;
     hipLaunchKernelGGL(k, dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N,
-                       k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr);
+                       k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr,
+                       nullptr);
     return;
   }
   auto k = one ? conv3x3_halo_kernel<T, BN, true> : conv3x3_halo_kernel<T, BN, false>;
@@ -2212,18 +2324,47 @@ bool conv3x3_x2_eligible(const GatherArg& g, int N) {
          conv3x3_x2_shape_ok(g.h, g.w, g.Ctot, g.src[0].C, N);
 }
 
+// SELUNET_OPT_TILE_QUEUE: the split-fp16 persistent kernel takes its pixel tiles from a ticket counter
+// (conv3x3_halo_persist_kernel, TQ) and flushes statistics per tile (slab rows = pixel tiles)
+bool x2_tile_queue() { return option(SELUNET_OPT_TILE_QUEUE, 0) != 0; }
+
+// the queue's counters: [2][n_tiles <= 64], zero between launches (each launch's last workgroups reset them);
+// allocated on first use on the current device (one process per GPU)
+static unsigned* tq_counters() {
+  static unsigned* p = nullptr;
+  if (p == nullptr) {
+    if (hipMalloc(&p, 128 * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 128 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+  }
+  return p;
+}
+
+// statistics slab rows of selunet_conv3x3_x2 (persistent kernel): workgroups per column tile, or pixel tiles
+int64_t conv3x3_x2_persist_rows(const GatherArg& g, int N) {
+  return x2_tile_queue() ? conv3x3_halo_tiles(g) : persist_rows(g, N);
+}
+
 template <int BN>
-static void launch_x2(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
-                      const float* amax1, hipStream_t st) {
+static int launch_x2(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                     const float* amax1, hipStream_t st) {
   const int tiles_x = (int)cdiv(g.w, TW), tiles_y = (int)cdiv(g.h, TH);
   const int n_tiles = N / BN;
-  const int gp = persist_rows(g, N);  // = the statistics slab rows of selunet_gemm_stats_rows
+  const int gp = persist_rows(g, N);  // workgroups per column tile (static: = the statistics slab rows)
   const int k_pad = 9 * g.Ctot;
   // 16x16x32 MFMAs at BN = 64 (1-4 % faster per layer); at BN = 128 they cost 20-25 % (the extra
   // fragment registers spill: 180 B of scratch per lane against 44) — DESIGN.md §3
+  if (x2_tile_queue()) {
+    unsigned* tq = tq_counters();
+    if (tq == nullptr || n_tiles > 64) return fail(SELUNET_ELAUNCH, "conv3x3_x2: tile-queue counters unavailable");
+    hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true, BN == 64, true>), dim3((unsigned)(gp * n_tiles)),
+                       dim3(HTHREADS), 0, st, g, w, N, k_pad, ep, n_tiles, tiles_x, tiles_y,
+                       (int)conv3x3_halo_tiles(g), gp, w + (int64_t)N * k_pad, amax0, amax1, tq);
+    return 0;
+  }
   hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true, BN == 64>), dim3((unsigned)(gp * n_tiles)),
                      dim3(HTHREADS), 0, st, g, w, N, k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g),
-                     gp, w + (int64_t)N * k_pad, amax0, amax1);
+                     gp, w + (int64_t)N * k_pad, amax0, amax1, nullptr);
+  return 0;
 }
 
 // 128-column tiles whenever N allows: unlike the Winograd kernel's register output transform, the
@@ -2236,8 +2377,9 @@ bool conv3x3_x2_bn128(int N, const EpiArg& ep) {
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st) {
   if (conv3x3_x2d_eligible(g, N)) return conv3x3_x2d_launch(g, w, ep, amax0, amax1, st);  // 64 columns
-  if (conv3x3_x2_bn128(N, ep)) launch_x2<128>(g, w, N, ep, amax0, amax1, st);
-  else launch_x2<64>(g, w, N, ep, amax0, amax1, st);
+  if (int rc = conv3x3_x2_bn128(N, ep) ? launch_x2<128>(g, w, N, ep, amax0, amax1, st)
+                                       : launch_x2<64>(g, w, N, ep, amax0, amax1, st))
+    return rc;
   return check_launch("conv3x3_x2");
 }
 

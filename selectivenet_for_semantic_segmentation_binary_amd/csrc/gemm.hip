@@ -1200,7 +1200,7 @@ extern "C" int64_t selunet_conv3x3_x2_stats_rows(const selunet_gather* a, int32_
   GatherArg g;
   if (make_gather(a, SELUNET_F32, g, 4)) return -1;
   if (conv3x3_x2d_eligible(g, n_cols)) return conv3x3_x2d_rows(g);
-  return conv3x3_halo_stats_rows(g, n_cols, SELUNET_F32);
+  return conv3x3_x2_persist_rows(g, n_cols);
 }
 
 extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
@@ -1221,6 +1221,7 @@ extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32
 }
 
 extern "C" int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols) {
+  if (x2_tile_queue()) return 0;  // the Winograd kernel keeps the static walk (its slab rows)
   // (measured slower than selunet_conv3x3_x2 on every UNet_B layer: off unless SELUNET_OPT_WX2 = 1)
   return option(SELUNET_OPT_WX2, 0) != 0 && halo_enabled() && conv3x3_x2_shape_ok(h, w, c_in, c_src0, n_cols) &&
                  conv3x3_wx2_shape_ok(h, w, c_in, c_src0, n_cols)
@@ -1561,6 +1562,34 @@ extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_g
   hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
                      (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
   return check_launch("conv3x3_wgrad_x2");
+}
+
+extern "C" int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                           float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                                           const selunet_bn_bwd_stats* bnb, const float* coef, float* dy, float* dy_amax,
+                                           void* stream) {
+  WgradPlan w;
+  if (int rc = plan_wgrad_x2(p, q, w)) return rc;
+  const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  SELUNET_REQUIRE(out != nullptr && ws != nullptr && ws_bytes >= need, "conv3x3_wgrad_x2_bn: out / workspace of %lld bytes",
+                  (long long)need);
+  SELUNET_REQUIRE(amax_p != nullptr && amax_q0 != nullptr && (q->nsrc == 1 || amax_q1 != nullptr),
+                  "conv3x3_wgrad_x2_bn: every operand source needs its range word");
+  SELUNET_REQUIRE(bnb && bnb->y && bnb->scale && bnb->shift && bnb->mean && bnb->invstd && coef,
+                  "conv3x3_wgrad_x2_bn: y, scale, shift, mean, invstd and coef are required");
+  SELUNET_REQUIRE(p->nsrc == 1 && p->src[0].scale == nullptr && p->src[0].layout == 0,
+                  "conv3x3_wgrad_x2_bn: p gathers dA alone (one source, no transform)");
+  SELUNET_REQUIRE(dy == nullptr || (dy != p->src[0].data && dy != bnb->y), "conv3x3_wgrad_x2_bn: dy must not alias dA or y");
+  SELUNET_REQUIRE((dy == nullptr) == (dy_amax == nullptr), "conv3x3_wgrad_x2_bn: dy and dy_amax go together");
+  const WgradBnArg bn{reinterpret_cast<const float*>(bnb->y), bnb->scale, bnb->shift, bnb->mean, bnb->invstd, coef, dy,
+                      dy_amax};
+  hipStream_t st = as_stream(stream);
+  if (int rc = conv3x3_wgrad_x2_launch(w.gp, w.gq, ws, w.nj_pad, amax_p, amax_q0, amax_q1, st, &bn)) return rc;
+  const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n4, 64), 16384));
+  hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
+                     (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
+  return check_launch("conv3x3_wgrad_x2_bn");
 }
 
 // generic fp32 weight gradient on split-fp16 operands (gemm_wgrad_x2_kernel + the fixed-order split

@@ -486,8 +486,23 @@ int conv3x3_x2d_launch(const GatherArg& g, const float* w, const EpiArg& ep, con
                        hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
 int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
+// SELUNET_OPT_TILE_QUEUE and the split-fp16 persistent kernel's statistics slab rows (conv3x3.hip)
+bool x2_tile_queue();
+int64_t conv3x3_x2_persist_rows(const GatherArg& g, int N);
+// the BN-backward apply fused into the split-fp16 weight gradient's dY staging (selunet_conv3x3_wgrad_x2_bn)
+struct WgradBnArg {
+  const float* y;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  const float* coef;
+  float* dy;
+  float* dy_amax;
+};
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
-                            const float* amax_q0, const float* amax_q1, hipStream_t st);
+                            const float* amax_q0, const float* amax_q1, hipStream_t st,
+                            const WgradBnArg* bn = nullptr);
 int conv3x3_wgrad_halo_launch(const GatherArg& p, const GatherArg& q, float* out, int ldo, float* ws, int dtype,
                               hipStream_t st);
 int64_t conv3x3_wgrad_halo_splits(const GatherArg& p, const GatherArg& q, int dtype, int64_t* per_out);

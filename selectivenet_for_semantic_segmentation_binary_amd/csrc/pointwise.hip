@@ -12,8 +12,8 @@ namespace selunet {
 // ------------------------------------------------------------------ error state, options
 static thread_local char g_err[512] = "";
 
-int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-static_assert(SELUNET_OPT_COUNT == 16, "g_options initialiser");
+int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(SELUNET_OPT_COUNT == 17, "g_options initialiser: one -1 per option");
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -484,6 +484,10 @@ struct BnbFinArgs {
   const float* gamma;
   const float* invstd;
   float *dgamma, *dbeta, *dbias, *coef;
+  // selunet_bn_bwd_stats_finalize_bound: atomic max of an upper bound of |dy| over the channels into
+  // *bound, from the exact max |dA| in *amax_da (the range word of the fused apply's dy operand)
+  const float* amax_da;
+  float* bound;
 };
 
 __device__ inline void bn_bwd_finalize_one(int c, int C, double sda, double sdax, double sx, const BnbFinArgs& a) {
@@ -497,6 +501,14 @@ __device__ inline void bn_bwd_finalize_one(int c, int C, double sda, double sdax
   a.coef[c] = (float)k0;
   a.coef[C + c] = (float)k1;
   a.coef[2 * C + c] = (float)k2;
+  if (a.bound) {
+    // dy = k0 da - k1 - k2 xhat with |da| <= |dA| <= amax_da and |xhat| <= sqrt(count - 1) (Samuelson:
+    // batch statistics; the fp32 mean / invstd and the rounding of dy are covered by the 1.25 margin).
+    // The split-fp16 operand needs an upper bound only: a loose one costs precision below 2^-17 of it
+    // (absolute error <= 2^-39 of the bound), far under fp32 rounding of the products it feeds
+    const double bnd = fabs(k0) * (double)a.amax_da[0] + fabs(k1) + fabs(k2) * sqrt((double)a.count);
+    atomicMax(reinterpret_cast<unsigned*>(a.bound), __float_as_uint((float)(1.25 * bnd)));
+  }
 }
 
 __global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, int C, BnbFinArgs a) {
@@ -1861,6 +1873,18 @@ int selunet_bn_bwd_stats_finalize(const float* slab, int64_t rows, double* ws, d
   const BnbFinArgs ba{count, gamma, invstd, dgamma, dbeta, dbias, coef};
   launch_reduce_finalize<3>(slab, rows, c, ws, sums, BnFinArgs{}, ba, as_stream(stream));
   return check_launch("bn_bwd_stats_finalize");
+}
+
+int selunet_bn_bwd_stats_finalize_bound(const float* slab, int64_t rows, double* ws, double* sums, int64_t count,
+                                        int32_t c, const float* gamma, const float* invstd, float* dgamma, float* dbeta,
+                                        float* dbias, float* coef, const float* amax_da, float* bound, void* stream) {
+  SELUNET_REQUIRE(slab && ws && rows > 0 && gamma && invstd && coef && c > 0 && count > 0 && amax_da && bound,
+                  "bn_bwd_stats_finalize_bound: bad arguments");
+  BnbFinArgs ba{count, gamma, invstd, dgamma, dbeta, dbias, coef};
+  ba.amax_da = amax_da;
+  ba.bound = bound;
+  launch_reduce_finalize<3>(slab, rows, c, ws, sums, BnFinArgs{}, ba, as_stream(stream));
+  return check_launch("bn_bwd_stats_finalize_bound");
 }
 
 int selunet_bn_bwd_reduce(const void* dz, const void* y, int64_t m, int32_t c, const float* scale, const float* shift,

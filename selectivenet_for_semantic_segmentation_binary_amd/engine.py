@@ -62,6 +62,7 @@ class BNState:
     w: int
     c: int
     amax: torch.Tensor = None  # range word of relu(bn(y)) (split-fp16 layers, selunet_act_bound)
+    name: str = ""
 
     def src(self):
         return K.source(self.y, self.c, self.scale, self.shift, relu=True, amax=self.amax)
@@ -90,6 +91,7 @@ class DGrad:
     slab: torch.Tensor = None
     rows: int = 0
     apply: object = None
+    da_word: bool = False  # the producer recorded max |t| in ctx.words["da:" + layer] (fused apply's bound)
 
 
 def bnb_for(st: BNState, slab) -> K.BnBwdStats:
@@ -153,6 +155,9 @@ class Engine:
         # SELUNET_BN_SHIFT=0 keeps c = 0
         self.bn_shift = dt == torch.float32 and BN_CENTER_RATIO is not None and \
             os.environ.get("SELUNET_BN_SHIFT", "1") != "0"
+        # split-fp16 training: the BN-backward apply of layers whose dA is stored runs inside their weight
+        # gradient (selunet_conv3x3_wgrad_x2_bn); SELUNET_FUSE_WGRAD_APPLY=0 keeps the separate apply
+        self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -400,7 +405,7 @@ class Engine:
                    K.ptr(P[f"{name}.1.bias"]), K.ptr(B[f"{name}.1.running_mean"]), K.ptr(B[f"{name}.1.running_var"]),
                    K.ptr(B[f"{name}.1.num_batches_tracked"]), BN_MOMENTUM, BN_EPS, 0,
                    K.ptr(mean), K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
-        st = BNState(y, mean, invstd, scale, shift, n, h, w, co)
+        st = BNState(y, mean, invstd, scale, shift, n, h, w, co, name=name)
         # range word of relu(bn(y)) for the split-fp16 consumers. The Samuelson bound |xhat| <= sqrt(M - 1)
         # holds for statistics over THIS rank's M values (per-rank BatchNorm, DataParallel replica
         # semantics); a synchronized BatchNorm would need M = the global count here.
@@ -514,7 +519,9 @@ class Engine:
         hw, hb = ctx.wpack.pop("heads")
         ctx.x2 = any(wp.mode in X2_MODES for wp in ctx.wpack.values())
         if ctx.x2:  # the operand range words of this step, zeroed for their atomic-max producers
-            keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy", "du")]
+            # act: relu(bn(y)); dy / du: conv-output and up-sampled gradients; da: the exact max |dA| its
+            # producer stores; dyb: the bound of |dy| selunet_bn_bwd_stats_finalize_bound derives from it
+            keys = [f"{k}:{nm}" for nm, _, _ in LY.CBR_LAYERS for k in ("act", "dy", "du", "da", "dyb")]
             keys += ["up:" + nm for nm, _, _ in LY.UNPOOLS]
             buf = K.keep(torch.empty(len(keys), dtype=torch.float32, device=x.device))
             K.call("selunet_memset", K.ptr(buf), 0, buf.numel() * 4, self.stream)
@@ -591,9 +598,27 @@ class Engine:
         coef = K.keep(torch.empty(3, co, dtype=torch.float32, device=dev))
         gamma = ctx.params[f"{name}.1.weight"]
         ws = K.keep(torch.empty(K.query("selunet_reduce_ws_bytes", 3 * co) // 8, dtype=torch.float64, device=dev))
-        K.call("selunet_bn_bwd_stats_finalize", K.ptr(dg.slab), dg.rows, K.ptr(ws), None, M, co, K.ptr(gamma),
-               K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]), K.ptr(G[f"{name}.0.bias"]),
-               K.ptr(coef), self.stream)
+        wp = ctx.wpack[name] if first_x is None else None
+        ci = sum(s.channels for s in input_srcs)
+        # the BN-backward apply fused into the split-fp16 weight gradient: dA's producer
+        # recorded max |dA|, the finalize turns it into a bound of |dy|, the weight gradient forms dy from
+        # (dA, y) while staging and writes it (with its exact max) for the data gradient
+        fuse = (wp is not None and wp.mode in X2_MODES and dg.apply is None and dg.t is not None and dg.da_word and
+                self.fuse_wgrad_apply and all(sr.amax is not None for sr in input_srcs))
+        gp = gq = None
+        if fuse:
+            gp = K.gather(st.n, st.h, st.w, 1, K.source(dg.t, co))
+            gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
+            fuse = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq) > 0
+        if fuse:
+            K.call("selunet_bn_bwd_stats_finalize_bound", K.ptr(dg.slab), dg.rows, K.ptr(ws), None, M, co, K.ptr(gamma),
+                   K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]),
+                   K.ptr(G[f"{name}.0.bias"]), K.ptr(coef), K.ptr(self._word(ctx, "da:" + name)),
+                   K.ptr(self._word(ctx, "dyb:" + name)), self.stream)
+        else:
+            K.call("selunet_bn_bwd_stats_finalize", K.ptr(dg.slab), dg.rows, K.ptr(ws), None, M, co, K.ptr(gamma),
+                   K.ptr(st.invstd), K.ptr(G[f"{name}.1.weight"]), K.ptr(G[f"{name}.1.bias"]),
+                   K.ptr(G[f"{name}.0.bias"]), K.ptr(coef), self.stream)
         if first_x is not None:
             # encoder_layer_1_1: its dy feeds only the weight gradient (the input needs none), which
             # forms it from dA and y while staging (selunet_first_conv_wgrad_bn): dy is never written
@@ -610,23 +635,31 @@ class Engine:
             K.marker(("grads", name))
             return None
         dy = K.keep(torch.empty(M, co, dtype=self.dt, device=dev))
-        wp = ctx.wpack[name]
         dyw = self._word(ctx, "dy:" + name) if wp.mode in X2_MODES else None
-        if dg.apply is not None:  # dA formed on the fly from its producer's inputs
-            dg.apply(dy, coef, dyw)
-        elif dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
-            K.call("selunet_bn_bwd_apply_amax", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
-                   K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.code, self.stream)
+        if fuse:
+            # weight gradient with the apply in its dY staging; it writes dy and max |dy| (dyw)
+            wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq)
+            wsx = K.keep(torch.empty(wsb // 4, dtype=torch.float32, device=dev))
+            words = [sr.amax for sr in input_srcs]
+            K.call("selunet_conv3x3_wgrad_x2_bn", gp, gq, K.ptr(wsx), wsb, K.ptr(G[f"{name}.0.weight"]),
+                   K.ptr(self._word(ctx, "dyb:" + name)), K.ptr(words[0]), K.ptr(words[1]) if len(words) > 1 else None,
+                   bnb_for(st, None), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.stream)
         else:
-            K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
-                   K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
-        # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
-        ci = sum(s.channels for s in input_srcs)
-        ld = K.query("selunet_wgrad_ld", q_taps * ci)
-        gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
-        gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
-        if not self._wgrad_x2(gp, gq, dyw, input_srcs, G[f"{name}.0.weight"]):
-            self._wgrad_param(gp, gq, K.WG_CONV3X3, co, ld, G[f"{name}.0.weight"])
+            if dg.apply is not None:  # dA formed on the fly from its producer's inputs
+                dg.apply(dy, coef, dyw)
+            elif dyw is not None:  # dy with its range word (the split-fp16 data gradient reads it)
+                K.call("selunet_bn_bwd_apply_amax", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale),
+                       K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), K.ptr(dyw),
+                       self.code, self.stream)
+            else:
+                K.call("selunet_bn_bwd_apply", K.ptr(dg.t), K.ptr(st.y), M, co, K.ptr(st.scale), K.ptr(st.shift),
+                       K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dy), self.code, self.stream)
+            # weight gradient: out[co][(tap, ci)] = sum_m dy[m][co] * X_im2col[m][(tap, ci)]
+            ld = K.query("selunet_wgrad_ld", q_taps * ci)
+            gp = K.gather(st.n, st.h, st.w, 1, K.source(dy, co))
+            gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
+            if not self._wgrad_x2(gp, gq, dyw, input_srcs, G[f"{name}.0.weight"]):
+                self._wgrad_param(gp, gq, K.WG_CONV3X3, co, ld, G[f"{name}.0.weight"])
         K.marker(("grads", name))
         if not need_dgrad:
             return None
@@ -642,8 +675,10 @@ class Engine:
             if prev is not None:
                 slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
                 ep.bnb = bnb_for(prev, slab)
+                if ctx.x2 and ("da:" + prev.name) in ctx.words:  # max |dA| for a fused apply's |dy| bound
+                    ep.amax = K.ptr(self._word(ctx, "da:" + prev.name))
             self._conv3x3(ga, wd, ci, 9 * co, ep, wp.mode, (dsrc,))
-            return DGrad(dx, slab, rows)
+            return DGrad(dx, slab, rows, da_word=ep.amax is not None)
         c0 = dgrad_split
         d0 = K.keep(torch.empty(M, c0, dtype=self.dt, device=dev))
         d1 = K.keep(torch.empty(M, ci - c0, dtype=self.dt, device=dev))
@@ -681,11 +716,15 @@ class Engine:
         slab = K.keep(torch.empty(rows, 3, ci, dtype=torch.float32, device=dev))
         ep = K.Epilogue(K.ptr(dz), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = bnb_for(prev, slab)
+        da_word = False
         if wp.mode == "x2":
+            if ("da:" + prev.name) in ctx.words:  # max |dA| for a fused apply's |dy| bound
+                ep.amax = K.ptr(self._word(ctx, "da:" + prev.name))
+                da_word = True
             K.call("selunet_gemm_gather_x2", ga, K.ptr(wd), ci, 4 * co, ep, K.ptr(duw), None, self.stream)
         else:
             K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
-        return DGrad(dz, slab, rows)
+        return DGrad(dz, slab, rows, da_word=da_word)
 
     def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
         rows = K.query("selunet_maxpool2_bwd_slab_rows", st.n, st.h, st.w, st.c)

@@ -167,3 +167,104 @@ def test_sums_only_needs_the_sums():
     with pytest.raises(RuntimeError):
         K.call("selunet_maxpool2_bwd", K.ptr(y), 1, 8, 8, 64, K.ptr(sc), K.ptr(sc), K.ptr(y), None, None, None, K.F32,
                K.stream_ptr())
+
+
+def _bn_state(m, c, seed):
+    """y with its real batch statistics (the Samuelson bound of selunet_bn_bwd_stats_finalize_bound holds
+    for those only), the forward's folded scale / shift, and a dA."""
+    g = torch.Generator().manual_seed(seed)
+    y = (torch.randn(m, c, generator=g, dtype=torch.float64) * (torch.rand(c, generator=g, dtype=torch.float64) + 0.2)
+         + torch.randn(c, generator=g, dtype=torch.float64))
+    mean, var = y.mean(0), y.var(0, unbiased=False)
+    invstd = 1.0 / torch.sqrt(var + 1e-5)
+    gamma = torch.randn(c, generator=g, dtype=torch.float64) * 0.5 + 1.0
+    beta = torch.randn(c, generator=g, dtype=torch.float64) * 0.2
+    sc, sh = gamma * invstd, beta - mean * gamma * invstd
+    da = torch.randn(m, c, generator=g, dtype=torch.float64) * 1e-3
+    f = lambda t: t.float().to(DEV).contiguous()  # noqa: E731
+    return f(y), f(mean), f(invstd), f(gamma), f(sc), f(sh), f(da)
+
+
+@pytest.mark.parametrize("c", [64, 256])
+def test_bn_bwd_finalize_bound_covers_dy(c):
+    """selunet_bn_bwd_stats_finalize_bound: the same coefficients and parameter gradients as
+    selunet_bn_bwd_stats_finalize, and a range word >= max |dy| of the apply they feed."""
+    m = 20000
+    y, mean, invstd, gamma, sc, sh, da = _bn_state(m, c, 5)
+    mask = (y * sc + sh > 0).float()
+    xh = (y - mean) * invstd
+    slab = torch.stack([(da * mask).sum(0), (da * mask * xh).sum(0), xh.sum(0)]).reshape(1, 3, c).contiguous()
+    ws = torch.empty(K.query("selunet_reduce_ws_bytes", 3 * c) // 8, dtype=torch.float64, device=DEV)
+    amax_da = da.abs().max().reshape(1).contiguous()
+    outs = []
+    for bound in (False, True):
+        coef, dg, db, dbias = (torch.empty(3, c, device=DEV), torch.empty(c, device=DEV), torch.empty(c, device=DEV),
+                               torch.empty(c, device=DEV))
+        word = torch.zeros(1, device=DEV)
+        if bound:
+            K.call("selunet_bn_bwd_stats_finalize_bound", K.ptr(slab), 1, K.ptr(ws), None, m, c, K.ptr(gamma),
+                   K.ptr(invstd), K.ptr(dg), K.ptr(db), K.ptr(dbias), K.ptr(coef), K.ptr(amax_da), K.ptr(word),
+                   K.stream_ptr())
+        else:
+            K.call("selunet_bn_bwd_stats_finalize", K.ptr(slab), 1, K.ptr(ws), None, m, c, K.ptr(gamma), K.ptr(invstd),
+                   K.ptr(dg), K.ptr(db), K.ptr(dbias), K.ptr(coef), K.stream_ptr())
+        outs.append((coef.cpu(), dg.cpu(), db.cpu(), dbias.cpu(), word.item()))
+    (c0, g0, b0, d0, _), (c1, g1, b1, d1, w1) = outs
+    assert torch.equal(c0, c1) and torch.equal(g0, g1) and torch.equal(b0, b1) and torch.equal(d0, d1)
+    dy = torch.empty(m, c, device=DEV)
+    am = torch.zeros(1, device=DEV)
+    K.call("selunet_bn_bwd_apply_amax", K.ptr(da), K.ptr(y), m, c, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+           K.ptr(c1.to(DEV)), K.ptr(dy), K.ptr(am), K.F32, K.stream_ptr())
+    torch.cuda.synchronize()
+    assert 0.0 < am.item() <= w1
+    print(f"bound / max|dy| = {w1 / am.item():.1f}")
+
+
+@pytest.mark.parametrize("co,ci", [(64, 64), (64, 128), (128, 128), (256, 64)])
+def test_wgrad_x2_bn_equals_apply_then_wgrad(co, ci):
+    """selunet_conv3x3_wgrad_x2_bn (the BN-backward apply in the weight gradient's dY staging) against
+    selunet_bn_bwd_apply_amax + selunet_conv3x3_wgrad_x2: dy and max |dy| identical (same arithmetic),
+    the weight gradient within split-fp16 rounding of it and of the fp64 weight gradient, although it
+    stages dy with a looser range word (a bound 37x the exact max)."""
+    n, h, w = 2, 20, 36  # ragged 8x8 tiles in y
+    m = n * h * w
+    y, mean, invstd, _, sc, sh, da = _bn_state(m, co, 7)
+    coef = (gen(3, co, seed=70) * 0.5).to(DEV).contiguous()
+    coef[0] = coef[0].abs() + 0.5
+    x = gen(m, ci, seed=71).to(DEV)
+    xsc, xsh = (gen(ci, seed=72).abs() + 0.5).to(DEV), (gen(ci, seed=73) * 0.2).to(DEV)
+    xw = (torch.relu(x * xsc + xsh)).abs().max().reshape(1).contiguous()
+    gq = K.gather(n, h, w, 9, K.source(x, ci, xsc, xsh, relu=True, amax=xw))
+    # unfused pair
+    dy0 = torch.empty(m, co, device=DEV)
+    am0 = torch.zeros(1, device=DEV)
+    K.call("selunet_bn_bwd_apply_amax", K.ptr(da), K.ptr(y), m, co, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+           K.ptr(coef), K.ptr(dy0), K.ptr(am0), K.F32, K.stream_ptr())
+    gp0 = K.gather(n, h, w, 1, K.source(dy0, co))
+    wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp0, gq)
+    assert wsb > 0
+    ws = torch.empty(wsb // 4, device=DEV)
+    dw0 = torch.empty(co, ci, 3, 3, device=DEV)
+    K.call("selunet_conv3x3_wgrad_x2", gp0, gq, K.ptr(ws), wsb, K.ptr(dw0), K.ptr(am0), K.ptr(xw), None, K.stream_ptr())
+    torch.cuda.synchronize()
+    # fused
+    bound = (am0 * 37.0).contiguous()
+    dy1 = torch.full((m, co), float("nan"), device=DEV)
+    am1 = torch.zeros(1, device=DEV)
+    dw1 = torch.empty(co, ci, 3, 3, device=DEV)
+    gp1 = K.gather(n, h, w, 1, K.source(da, co))
+    bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), None)
+    K.call("selunet_conv3x3_wgrad_x2_bn", gp1, gq, K.ptr(ws), wsb, K.ptr(dw1), K.ptr(bound), K.ptr(xw), None, bnb,
+           K.ptr(coef), K.ptr(dy1), K.ptr(am1), K.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dy1.cpu(), dy0.cpu())
+    assert am1.item() == am0.item()
+    # fp64 weight gradient of dy0 against relu(x sc + sh)
+    xin = torch.relu(x.double() * xsc.double() + xsh.double()).reshape(n, h, w, ci).permute(0, 3, 1, 2)
+    g = dy0.double().reshape(n, h, w, co).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xin.cpu(), (co, ci, 3, 3), g.cpu(), padding=1)
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())  # noqa: E731
+    e0, e1 = rel(dw0.cpu(), ref), rel(dw1.cpu(), ref)
+    print(f"wgrad rel err unfused {e0:.2e} fused {e1:.2e}")
+    assert e1 < 2e-6 and e0 < 2e-6
+    assert rel(dw1.cpu(), dw0.cpu().double()) < 2e-6

@@ -202,13 +202,31 @@ def test_eval_forward_and_metrics():
         o, s, a = net(torch.tensor(d["x"], device=DEV))
     o, s = o.cpu().numpy(), s.cpu().numpy()
     assert G.max_rel(o, d["output"]) < 1e-4 and G.max_rel(s, d["selection"]) < 1e-4
-    pred = O.eval_pred_mask(o)
-    flips = pred != d["pred"]
-    assert np.abs(d["output"][flips]).max(initial=0) < 1e-4 * np.abs(d["output"]).max()
-    if not flips.any():
-        cm = O.confusion_matrix(d["label"].astype("uint8"), pred, selection=O.eval_pred_mask(s))
+    # eval masks (fp32 sigmoid > 0.5) of both heads; a mask bit may differ from the reference's only where
+    # the reference logit lies within the logit error this run measures on the other pixels (the
+    # training steps' rule, tests/_golden.py::mask_flips), capped at 1e-4 of the largest |logit|
+    label = d["label"].astype("uint8")
+    pred, sel = O.eval_pred_mask(o), O.eval_pred_mask(s)
+    ref_pred, ref_sel = d["pred"].astype("uint8"), O.eval_pred_mask(d["selection"])
+    flipped = []
+    for ours_l, ref_l, ours_m, ref_m in ((o, d["output"], pred, ref_pred), (s, d["selection"], sel, ref_sel)):
+        diff = ours_m != ref_m
+        err = np.abs(ours_l.astype(np.float64) - ref_l)
+        e_meas = float(err[~diff].max(initial=0.0))
+        if diff.any():
+            worst = float(np.abs(ref_l[diff]).max())
+            assert worst <= min(e_meas, 1e-4 * float(np.abs(ref_l).max())), (int(diff.sum()), worst, e_meas)
+        flipped.append(diff)
+    keep = ~(flipped[0] | flipped[1])
+    # the confusion matrix is compared in every case: over the pixels outside the allowed flips it must be
+    # the reference's exactly; with no flips that is the fixture's whole selective matrix and mIoU
+    cm_keep = O.confusion_matrix(label[keep], pred[keep], selection=sel[keep])
+    assert np.array_equal(cm_keep, O.confusion_matrix(label[keep], ref_pred[keep], selection=ref_sel[keep]))
+    cm = O.confusion_matrix(label, pred, selection=sel)
+    assert np.abs(cm - d["eval_cm_selective"]).sum() <= 2 * int((~keep).sum())
+    if keep.all():
         assert np.array_equal(cm, d["eval_cm_selective"])
-        assert abs(O.miou(cm) - float(d["eval_miou_selective"])) < 0.002
+    assert abs(O.miou(cm) - float(d["eval_miou_selective"])) < 0.002
 
 
 def test_bf16_step_tracks_fp32():

@@ -33,6 +33,18 @@ def x2d():
         K.set_option("X2D", v)
 
 
+@pytest.fixture
+def tile_queue():
+    """Set SELUNET_OPT_TILE_QUEUE for one test (1: tiles from a ticket counter, statistics per tile)."""
+    prev = []
+
+    def setter(mode):
+        prev.append(K.set_option("TILE_QUEUE", mode))
+    yield setter
+    for v in prev[:1]:
+        K.set_option("TILE_QUEUE", v)
+
+
 def pack_x2(w, dgrad=True):
     """Split-fp16 operands of a conv3x3 weight [co][ci][3][3] through selunet_pack_weights: fwd
     [co][9*ci] words + co unscale factors, dgrad [ci][9*co] + ci."""
@@ -95,10 +107,11 @@ def word(v):
     (64, 64, 64, 1, 40, 72, True),      # 64 columns, two sources, partial tiles, four chunks
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
-@pytest.mark.parametrize("x2d_mode", [1, 0])
-def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, halo_wgs, x2d):
+@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1)])
+def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, tq, halo_wgs, x2d, tile_queue):
     halo_wgs(wgs)
     x2d(x2d_mode)
+    tile_queue(tq)
     x0 = gen(n, cin0, h, w, seed=1)
     x1 = gen(n, cin1, h, w, seed=2) * 1e-3 if cin1 else None  # sources of different ranges
     wt = gen(cout, cin0 + cin1, 3, 3, seed=3, scale=0.05)
@@ -139,11 +152,12 @@ def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, halo_wgs,
                                                 (512, 256, 256, 16, 16), (64, 64, 0, 64, 48),
                                                 (64, 128, 0, 48, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
-@pytest.mark.parametrize("x2d_mode", [1, 0])
-def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, halo_wgs, x2d):
+@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1)])
+def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, tq, halo_wgs, x2d, tile_queue):
     """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range."""
     halo_wgs(wgs)
     x2d(x2d_mode)
+    tile_queue(tq)
     n = 2
     wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
     dy = gen(n, cout, h, w, seed=7) * 1e-9
@@ -176,6 +190,43 @@ def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, halo_wgs, x2d):
         check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
     torch.cuda.synchronize()
     assert rel(got, ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(128, 128, 2, 40, 48), (256, 64, 1, 32, 80)])
+def test_x2_tile_queue_is_schedule_independent(cin, cout, n, h, w, halo_wgs, x2d, tile_queue):
+    """SELUNET_OPT_TILE_QUEUE: pixel tiles taken from a ticket counter, statistics flushed per tile into slab
+    row = tile index, so the outputs, the BN-backward sums and the range word are bit-identical whichever
+    workgroup ran a tile — here under three workgroup counts (and so three assignments) and two repeats
+    (the counters reset themselves between launches)."""
+    x2d(0)
+    tile_queue(1)
+    wt = gen(cout, cin, 3, 3, seed=6, scale=0.05)
+    dy = nhwc(gen(n, cout, h, w, seed=7) * 1e-6).to(DEV)
+    _, dg = pack_x2(wt)
+    M = n * h * w
+    am = word(dy.abs().max())
+    g = K.gather(n, h, w, 9, K.source(dy, cout))
+    rows = K.query("selunet_conv3x3_x2_stats_rows", g, cin)
+    assert rows == n * ((h + 15) // 16) * ((w + 15) // 16)  # one slab row per pixel tile
+    yprev = gen(M, cin, seed=42).to(DEV)
+    sc, sh = (gen(cin, seed=43).abs() + 0.5).to(DEV), (gen(cin, seed=44) * 0.3).to(DEV)
+    mean, invstd = (gen(cin, seed=45) * 0.1).to(DEV), (gen(cin, seed=46).abs() + 0.5).to(DEV)
+    outs = []
+    for wgs in (0, 3, 7, 0):
+        halo_wgs(wgs)
+        dx = torch.empty(M, cin, device=DEV)
+        slab = torch.full((rows, 3, cin), float("nan"), device=DEV)
+        amax = torch.zeros(1, device=DEV)
+        ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
+        ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+        ep.amax = K.ptr(amax)
+        K.call("selunet_conv3x3_x2", g, K.ptr(dg), cin, ep, K.ptr(am), None, K.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((dx.cpu(), slab.cpu(), amax.item()))
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1]) and o[2] == outs[0][2]
+    assert not torch.isnan(outs[0][1]).any()
+    check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
 
 
 def test_x2_rejects():

@@ -1,0 +1,127 @@
+"""Where does decoder_layer_4_2.1.bias's gradient error come from? (GPU, study tool)
+
+At the benchmarked shape (batch 128, 256x256, the step_sel_n128_256 fixture's seeds) the HIP fp32
+step's worst gradient against fp64 is decoder_layer_4_2's BN beta gradient, 1.33x the reference fp32
+step's own error, on both fp32 conv paths. That gradient is sum over pixels of da = dA * relu'(bn(y)),
+formed from the BN-backward sums the data gradient of decoder_layer_4_1 accumulates in its epilogue
+(model.py:87-88: decoder_layer_4_2 is the first bottleneck block, 4_1 the second). This tool runs
+  * the oracle (oracle/unet_b_cpu.py, the checker) in fp64 on the GPU with the CBR outputs' gradients
+    retained: the truth dA and the truth beta gradient;
+  * the engine's step with dA of decoder_layer_4_2 captured (SELUNET_NO_PLANS=1, a wrapper around
+    Engine._cbr_bwd), and its beta gradient;
+and prints the relative errors of: the engine's dA (masked) against fp64, the engine's beta gradient,
+and the fp64 sum of the engine's own captured da — so the summation (epilogue partial sums, slab
+reduction) is separated from the error of the dA values it sums. It repeats the split at every CBR
+block, so the layer is seen next to the others.
+
+    SELUNET_NO_PLANS=1 python tools/bias_error.py [--n 128]
+"""
+import argparse
+import os
+import sys
+
+os.environ["SELUNET_NO_PLANS"] = "1"
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import selectivenet_for_semantic_segmentation_binary_amd as S  # noqa: E402
+import selectivenet_for_semantic_segmentation_binary_amd.layout as L  # noqa: E402
+from selectivenet_for_semantic_segmentation_binary_amd import engine as E  # noqa: E402
+from oracle import unet_b_cpu as O  # noqa: E402  (the checker)
+from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a - b).norm() / max(float(b.norm()), 1e-300))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=128)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--data-seed", type=int, default=-1, help="-1: the step_sel_n128_256 fixture's")
+    a = ap.parse_args()
+    data_seed = a.data_seed
+    if data_seed < 0:
+        d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                                 "step_sel_n128_256.npz"), allow_pickle=False)
+        data_seed = int(d["meta_data_seed"])
+    dev = torch.device("cuda")
+    x, lab = make_batch(a.n, a.size, seed=data_seed)
+    layers = [nm for nm, _, _ in L.CBR_LAYERS]
+
+    # ---- ours: capture dA of every CBR block and its BN state
+    cap = {}
+    orig = E.Engine._cbr_bwd
+
+    def wrapped(self, ctx, name, dg, G, input_srcs, **kw):
+        st = ctx.bn[name]
+        if dg.t is not None:
+            cap[name] = (dg.t.detach().clone(), st.y.detach().clone(), st.scale.clone(), st.shift.clone())
+        else:  # producer in sums-only mode (heads / pools): dA is formed inside the apply, not stored
+            cap[name] = None
+        return orig(self, ctx, name, dg, G, input_srcs, **kw)
+
+    E.Engine._cbr_bwd = wrapped
+    net = S.UNet_B("RGB", selective=True)
+    p = L.seeded_params(a.seed, "RGB", True)
+    with torch.no_grad():
+        for k, t in net.named_parameters():
+            t.copy_(torch.tensor(p[k]))
+    net = net.to(dev).train()
+    xt, lt = torch.tensor(x, device=dev), torch.tensor(lab, device=dev)
+    out, sel, aux = net(xt)
+    loss = S.BCEWithLogitsLoss()(aux, lt) + S.calc_selective_risk_image_b(out, sel, target=lt, lamb=2)[0]
+    loss.backward()
+    torch.cuda.synchronize()
+    ours_g = {k: q.grad.detach().double().cpu() for k, q in net.named_parameters()}
+    E.Engine._cbr_bwd = orig
+    del net, out, sel, aux, loss
+    torch.cuda.empty_cache()
+
+    # ---- fp64 oracle with every CBR output's gradient retained
+    zs = {}
+    ocbr = O._cbr
+
+    def rec(params, buffers, name, t, training):
+        z = ocbr(params, buffers, name, t, training)
+        z.retain_grad()
+        zs[name] = z
+        return z
+
+    O._cbr = rec
+    params, buffers = O.make_state(a.seed, "RGB", selective=True)
+    params = type(params)((k, v.detach().to(dev, torch.float64).requires_grad_()) for k, v in params.items())
+    buffers = {k: (v.to(dev, torch.float64) if v.is_floating_point() else v.to(dev)) for k, v in buffers.items()}
+    opt = O.AdamRef(params.values(), lr=1e-3)
+    r = O.train_step(params, buffers, opt, torch.tensor(x, dtype=torch.float64, device=dev),
+                     torch.tensor(lab, dtype=torch.float64, device=dev), selective=True, lamb=2)
+    O._cbr = ocbr
+    g64 = {k: v.detach().double().cpu() for k, v in r["grads"].items()}
+    print(f"loss ours {float(r['loss']):.9f} (fp64)", flush=True)
+    print(f"{'layer':22s} {'dA err':>9s} {'beta err':>9s} {'sum(own da) err':>16s} {'|sum da|/sum|da|':>17s}")
+    for nm in layers:
+        z = zs[nm]
+        dz64 = z.grad.detach()  # [N, C, H, W] fp64
+        mask64 = (z.detach() > 0).double()
+        da64 = (dz64 * mask64).permute(0, 2, 3, 1).reshape(-1, z.shape[1])
+        beta64 = g64[f"{nm}.1.bias"]
+        cancel = float(beta64.abs().sum() / da64.abs().sum(0).sum().cpu()) if da64.numel() else 0.0
+        eb = rel(ours_g[f"{nm}.1.bias"], beta64)
+        if cap.get(nm) is None:
+            print(f"{nm:22s} {'(fused)':>9s} {eb:9.2e} {'-':>16s} {cancel:17.2e}")
+            continue
+        dA, y, sc, sh = cap[nm]
+        mask = ((y * sc + sh) > 0).double()
+        da = dA.double() * mask
+        e_da = rel(da, da64)
+        e_sum = rel(da.sum(0).cpu(), beta64)
+        print(f"{nm:22s} {e_da:9.2e} {eb:9.2e} {e_sum:16.2e} {cancel:17.2e}", flush=True)
+        del dA, y, da
+
+
+if __name__ == "__main__":
+    main()
