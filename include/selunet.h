@@ -386,10 +386,11 @@ int selunet_bn_stats_finalize(const float* slab, int64_t rows, double* ws, doubl
                               float* shift, void* stream);
 /* Second (centered) pass of the batch statistics, fp32 parity configuration: slab [rows][2][c] of
  * per-channel sums of (y - center) and (y - center)^2 over y [m][c] (center = the first pass's
- * batch mean; rows = selunet_channel_slab_rows(m)); then selunet_bn_stats_finalize_centered
+ * batch mean; rows = selunet_bn_centered_rows(m)); then selunet_bn_stats_finalize_centered
  * reduces it like selunet_bn_stats_finalize (mean = center + E[y - center], var = E[(y - center)^2]
  * - E[y - center]^2) and writes the same outputs — `mean` may alias `center`. Same role as
  * selunet_bn_stats_finalize (model.py:12 BatchNorm2d batch statistics), numerically two-pass. */
+int64_t selunet_bn_centered_rows(int64_t m);
 int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab,
                                  int32_t dtype, void* stream);
 /* Adaptive second pass: uvar[c] = the first pass's unbiased variance (selunet_bn_stats_finalize with

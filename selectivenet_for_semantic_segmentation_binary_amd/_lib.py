@@ -115,6 +115,7 @@ SIGNATURES = {
     "selunet_reduce_ws_bytes": (c_int64, [c_int32]),
     "selunet_reduce_rows": (c_int32, [P, c_int64, c_int32, P, P, P, P]),
     "selunet_channel_slab_rows": (c_int64, [c_int64]),
+    "selunet_bn_centered_rows": (c_int64, [c_int64]),
     "selunet_channel_sum": (c_int32, [P, c_int64, c_int32, P, c_int32, P]),
     "selunet_bn_finalize": (c_int32, [P, c_int64, c_int32, P, P, P, P, P, P, c_float, c_float, c_int32, P, P, P, P,
                                       P]),

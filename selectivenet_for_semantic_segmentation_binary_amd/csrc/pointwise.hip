@@ -308,6 +308,10 @@ __global__ void reduce_rows_l2(const double* __restrict__ ws, int splits, int co
 // before the fixed-order fp64 reduction of the slab (2048 blocks: 256 — the per-channel sums
 // here, e.g. the BN-backward sum of dA, cancel, so long fp32 runs cost digits)
 int64_t channel_slab_rows(int64_t m) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(m, 256), 8192)); }
+// rows (= blocks) of the centered second pass: after the first step it re-reads almost nothing (the shifted
+// first pass flags few channels), so its launch is mostly blocks that write a zero row — 512 of them instead
+// of up to 8192 (0.77 -> ~0.1 ms per bs=128 step); a re-read still streams at 8 waves per CU
+int64_t bn_centered_rows(int64_t m) { return std::min<int64_t>(channel_slab_rows(m), 512); }
 
 // Per-channel reduction skeleton over an NHWC [m][C] range: PL pixel lanes x (C/4) channel groups.
 // C in {64,128,256,512}.
@@ -1766,6 +1770,7 @@ int selunet_reduce_rows(const float* slab, int64_t rows, int32_t cols, double* w
 }
 
 int64_t selunet_channel_slab_rows(int64_t m) { return channel_slab_rows(m); }
+int64_t selunet_bn_centered_rows(int64_t m) { return bn_centered_rows(m); }
 
 int selunet_channel_sum(const void* x, int64_t m, int32_t c, float* slab, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(x && slab && m > 0 && ok_channels(c), "channel_sum: bad arguments (C=%d)", c);
@@ -1824,7 +1829,7 @@ int selunet_bn_stats_finalize_shifted(const float* slab, int64_t rows, double* w
 int selunet_bn_centered_partials(const void* y, int64_t m, int32_t c, const float* center, float* slab, int32_t dtype,
                                  void* stream) {
   SELUNET_REQUIRE(y && center && slab && m > 0 && ok_channels(c), "bn_centered_partials: bad arguments (C=%d)", c);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)bn_centered_rows(m)), dim3(TPB),
                                        0, as_stream(stream), (const T*)y, m, c, center, nullptr, 0.0f, slab));
   return check_launch("bn_centered_partials");
 }
@@ -1833,7 +1838,7 @@ int selunet_bn_centered_partials_adaptive(const void* y, int64_t m, int32_t c, c
                                           float ratio, float* slab, int32_t dtype, void* stream) {
   SELUNET_REQUIRE(y && center && uvar && slab && m > 1 && ok_channels(c) && ratio >= 0.0f,
                   "bn_centered_partials_adaptive: bad arguments (C=%d)", c);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_centered_partials_kernel<T>, dim3((unsigned)bn_centered_rows(m)), dim3(TPB),
                                        0, as_stream(stream), (const T*)y, m, c, center, uvar, ratio, slab));
   return check_launch("bn_centered_partials_adaptive");
 }

@@ -157,7 +157,7 @@ class Engine:
             os.environ.get("SELUNET_BN_SHIFT", "1") != "0"
         # split-fp16 training: the BN-backward apply of layers whose dA is stored runs inside their weight
         # gradient (selunet_conv3x3_wgrad_x2_bn); SELUNET_FUSE_WGRAD_APPLY=0 keeps the separate apply
-        self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "1") != "0"
+        self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "0") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -377,7 +377,7 @@ class Engine:
                        K.ptr(P[f"{name}.0.bias"]), K.ptr(P[f"{name}.1.weight"]), K.ptr(P[f"{name}.1.bias"]),
                        None, K.ptr(uvar), None, 1.0 if uvar is not None else BN_MOMENTUM, BN_EPS, K.ptr(mean),
                        K.ptr(invstd), K.ptr(scale), K.ptr(shift), self.stream)
-            rows2 = K.query("selunet_channel_slab_rows", M)
+            rows2 = K.query("selunet_bn_centered_rows", M)
             slab2 = K.keep(torch.empty(rows2, 2, co, dtype=torch.float32, device=dev))
             if uvar is not None:  # (shifted: the flags decide, ratio +inf)
                 K.call("selunet_bn_centered_partials_adaptive", K.ptr(y), M, co, K.ptr(mean), K.ptr(uvar),

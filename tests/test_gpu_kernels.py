@@ -804,7 +804,7 @@ def test_bn_adaptive_centered_variance(c):
     means = torch.where(tiny, 3e-3, means)
     stds = torch.where(tiny, 3.16e-5, 1.0)
     y = (torch.randn(M, c, generator=g, dtype=torch.float64) * stds + means).float().to(DEV)
-    rows = K.query("selunet_channel_slab_rows", M)
+    rows = K.query("selunet_bn_centered_rows", M)
     slab1 = torch.zeros(1, 2, c, device=DEV)
     slab1[0, 0] = y.double().sum(0).float()          # the conv epilogue's one-pass sums (fp32 slab)
     slab1[0, 1] = (y.double() ** 2).sum(0).float()
