@@ -96,7 +96,7 @@ class KernelTimer:
 
     MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
             "selunet_conv3x3_wx2",
-            "selunet_conv3x3_wgrad_x2", "selunet_gemm_wgrad_x2",
+            "selunet_conv3x3_wgrad_x2", "selunet_conv3x3_wgrad_x2_bn", "selunet_gemm_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
@@ -170,6 +170,12 @@ class KernelTimer:
             flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work
             nbytes = self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             return kname, "mfma_f16", flops, nbytes, f"wgrad x2 {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
+        if name == "selunet_conv3x3_wgrad_x2_bn":  # the BN-backward apply fused: reads dA and y, writes dy
+            gp, gq = args[0], args[1]
+            kname = f"conv3x3_wgrad_x2_bn<{128 if self._k(gp) % 128 == 0 else 64}>+reduce"
+            flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
+            nbytes = 3 * self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
+            return kname, "mfma_f16", flops, nbytes, f"wgrad x2 bn {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
         if name == "selunet_gemm_wgrad_x2":  # (gp, gq, ws, wsb, layout, out, amax_p0, p1, q0, q1, stream)
             gp, gq = args[0], args[1]
             flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work

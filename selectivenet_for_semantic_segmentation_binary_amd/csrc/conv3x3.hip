@@ -1324,7 +1324,7 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
 
   __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][XPIX][LDP];  // [buffer][h, l][pixel][co]
   __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][XHP][LDX];   // [buffer][h, l][halo pixel][ci]
-  __shared__ float Ks[KX + 2 * 64];
+  __shared__ __attribute__((aligned(16))) float Ks[KX + 2 * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1458,13 +1458,16 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
       if constexpr (BNA) {
         // dy of 4 channels (bn_bwd_apply_kernel's arithmetic), written once by channel chunk 0
         const float g[4] = {rp[r].x, rp[r].y, rp[r].z, rp[r].w}, yv[4] = {ry[r].x, ry[r].y, ry[r].z, ry[r].w};
+        // the 4 channels' coefficients: one 16-B LDS read per coefficient row
+        const f32x4 csc = *reinterpret_cast<const f32x4*>(Ks + cc * 4);
+        const f32x4 csh = *reinterpret_cast<const f32x4*>(Ks + BI + cc * 4);
+        const f32x4 ck0 = *reinterpret_cast<const f32x4*>(Ks + 2 * BI + cc * 4);
+        const f32x4 ca = *reinterpret_cast<const f32x4*>(Ks + 3 * BI + cc * 4);
+        const f32x4 cb = *reinterpret_cast<const f32x4*>(Ks + 4 * BI + cc * 4);
         float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int c = cc * 4 + e;
-          o[e] = (yv[e] * Ks[c] + Ks[BI + c] > 0.0f ? Ks[2 * BI + c] * g[e] : 0.0f) - Ks[4 * BI + c] -
-                 Ks[3 * BI + c] * yv[e];
-        }
+        for (int e = 0; e < 4; ++e)
+          o[e] = (yv[e] * csc[e] + csh[e] > 0.0f ? ck0[e] * g[e] : 0.0f) - cb[e] - ca[e] * yv[e];
         const float4 d = in ? make_float4(o[0], o[1], o[2], o[3]) : make_float4(0, 0, 0, 0);
         if (dy_out && in) {
           const int64_t off = (((int64_t)img * H + y0 + px / XTW) * W + x0 + px % XTW) * pa.C + i0 + cc * 4;

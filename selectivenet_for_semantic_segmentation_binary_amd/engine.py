@@ -157,7 +157,7 @@ class Engine:
             os.environ.get("SELUNET_BN_SHIFT", "1") != "0"
         # split-fp16 training: the BN-backward apply of layers whose dA is stored runs inside their weight
         # gradient (selunet_conv3x3_wgrad_x2_bn); SELUNET_FUSE_WGRAD_APPLY=0 keeps the separate apply
-        self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "0") != "0"
+        self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers

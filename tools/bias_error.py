@@ -79,6 +79,7 @@ def main():
     torch.cuda.synchronize()
     ours_g = {k: q.grad.detach().double().cpu() for k, q in net.named_parameters()}
     E.Engine._cbr_bwd = orig
+    print("engine step done", flush=True)
     del net, out, sel, aux, loss
     torch.cuda.empty_cache()
 
@@ -99,27 +100,66 @@ def main():
     opt = O.AdamRef(params.values(), lr=1e-3)
     r = O.train_step(params, buffers, opt, torch.tensor(x, dtype=torch.float64, device=dev),
                      torch.tensor(lab, dtype=torch.float64, device=dev), selective=True, lamb=2)
+    r_loss = float(r["loss"])
     O._cbr = ocbr
     g64 = {k: v.detach().double().cpu() for k, v in r["grads"].items()}
-    print(f"loss ours {float(r['loss']):.9f} (fp64)", flush=True)
-    print(f"{'layer':22s} {'dA err':>9s} {'beta err':>9s} {'sum(own da) err':>16s} {'|sum da|/sum|da|':>17s}")
+    da64s, mask64s = {}, {}
     for nm in layers:
         z = zs[nm]
-        dz64 = z.grad.detach()  # [N, C, H, W] fp64
-        mask64 = (z.detach() > 0).double()
-        da64 = (dz64 * mask64).permute(0, 2, 3, 1).reshape(-1, z.shape[1])
+        mask64s[nm] = (z.detach() > 0).permute(0, 2, 3, 1).reshape(-1, z.shape[1])
+        da64s[nm] = (z.grad.detach() * (z.detach() > 0)).permute(0, 2, 3, 1).reshape(-1, z.shape[1])
+    del zs, r, params, buffers, opt
+    torch.cuda.empty_cache()
+    print("fp64 oracle step done", flush=True)
+
+    # ---- the same oracle in fp32 (torch's own GPU kernels: a third fp32 implementation of the reference step)
+    zs32 = {}
+
+    def rec32(params, buffers, name, t, training):
+        z = ocbr(params, buffers, name, t, training)
+        z.retain_grad()
+        zs32[name] = z
+        return z
+
+    O._cbr = rec32
+    p32, b32 = O.make_state(a.seed, "RGB", selective=True)
+    p32 = type(p32)((k, v.detach().to(dev, torch.float32).requires_grad_()) for k, v in p32.items())
+    b32 = {k: (v.to(dev, torch.float32) if v.is_floating_point() else v.to(dev)) for k, v in b32.items()}
+    r32 = O.train_step(p32, b32, O.AdamRef(p32.values(), lr=1e-3), torch.tensor(x, device=dev),
+                       torch.tensor(lab, device=dev), selective=True, lamb=2)
+    O._cbr = ocbr
+    g32 = {k: v.detach().double().cpu() for k, v in r32["grads"].items()}
+    print("fp32 oracle step done", flush=True)
+
+    print(f"loss (fp64) {float(r_loss):.9f}", flush=True)
+    print("per CBR block: relative L2 error against the fp64 oracle of dA (masked: da = dA relu'), of the BN beta\n"
+          "gradient (= sum of da), of the fp64 sum of the engine's own da (the summation's share), the number of\n"
+          "ReLU-mask flips, and the dA error without the flipped pixels; the same for torch-fp32 (the oracle on the GPU)")
+    print(f"{'layer':22s} {'dA err':>9s} {'beta err':>9s} {'sum(own)':>9s} {'flips':>8s} {'dA err nf':>9s} | "
+          f"{'fp32 dA':>9s} {'fp32 beta':>9s} {'flips':>8s} {'dA err nf':>9s} | {'|sum da|/sum|da|':>16s}")
+    for nm in layers:
+        da64, m64 = da64s[nm], mask64s[nm]
         beta64 = g64[f"{nm}.1.bias"]
-        cancel = float(beta64.abs().sum() / da64.abs().sum(0).sum().cpu()) if da64.numel() else 0.0
+        cancel = float(beta64.abs().sum() / da64.abs().sum(0).sum().cpu())
         eb = rel(ours_g[f"{nm}.1.bias"], beta64)
+        z32 = zs32[nm]
+        m32 = (z32.detach() > 0).permute(0, 2, 3, 1).reshape(-1, z32.shape[1])
+        da32 = (z32.grad.detach() * (z32.detach() > 0)).permute(0, 2, 3, 1).reshape(-1, z32.shape[1]).double()
+        f32 = m32 != m64
+        e32, eb32, nf32 = rel(da32, da64), rel(g32[f"{nm}.1.bias"], beta64), int(f32.sum())
+        e32nf = rel(da32[~f32], da64[~f32])
         if cap.get(nm) is None:
-            print(f"{nm:22s} {'(fused)':>9s} {eb:9.2e} {'-':>16s} {cancel:17.2e}")
+            print(f"{nm:22s} {'(fused)':>9s} {eb:9.2e} {'-':>9s} {'-':>8s} {'-':>9s} | {e32:9.2e} {eb32:9.2e} "
+                  f"{nf32:8d} {e32nf:9.2e} | {cancel:16.2e}", flush=True)
             continue
         dA, y, sc, sh = cap[nm]
-        mask = ((y * sc + sh) > 0).double()
+        mask = (y * sc + sh) > 0
         da = dA.double() * mask
-        e_da = rel(da, da64)
-        e_sum = rel(da.sum(0).cpu(), beta64)
-        print(f"{nm:22s} {e_da:9.2e} {eb:9.2e} {e_sum:16.2e} {cancel:17.2e}", flush=True)
+        fl = mask != m64
+        e_da, e_sum, nfl = rel(da, da64), rel(da.sum(0).cpu(), beta64), int(fl.sum())
+        e_nf = rel(da[~fl], da64[~fl])
+        print(f"{nm:22s} {e_da:9.2e} {eb:9.2e} {e_sum:9.2e} {nfl:8d} {e_nf:9.2e} | {e32:9.2e} {eb32:9.2e} "
+              f"{nf32:8d} {e32nf:9.2e} | {cancel:16.2e}", flush=True)
         del dA, y, da
 
 
