@@ -117,8 +117,16 @@ def _miou_data(d):
             preprocess(*gen(int(d["meta_n_val"]), int(d["meta_val_seed"]))))
 
 
-MIOU_FIXTURES = [f for f in ("miou_sel_256s.npz", "miou_sel_256h.npz", "miou_sel_256.npz")
-                 if os.path.exists(os.path.join(G.GOLDEN, f))]
+def _has_ensemble(f):
+    """A fixture is a parity gate once its reference ensemble (`val_miou_ens`) has been collected."""
+    p = os.path.join(G.GOLDEN, f)
+    if not os.path.exists(p):
+        return False
+    with np.load(p, allow_pickle=False) as d:
+        return "val_miou_ens" in d.files
+
+
+MIOU_FIXTURES = [f for f in ("miou_sel_256s.npz", "miou_sel_256h.npz", "miou_sel_256.npz") if _has_ensemble(f)]
 
 
 @pytest.mark.parametrize("fname", MIOU_FIXTURES)
@@ -163,7 +171,7 @@ def test_miou_parity_vs_reference_training(dtype, tol, fname):
     print(line)
     G.SUMMARY.append(line)
     assert spread and max(spread.values()) < 0.002, ("the reference's own spread must sit inside the bar", spread)
-    if fname != "miou_sel_256.npz":  # the discriminative sets carry >= 8 reference members
+    if "ens_members" in d.files:  # collected by make_golden.py miou256x_collect: >= 8 reference members
         assert d["val_miou_ens"].size >= 8, d["val_miou_ens"].size
     assert abs(m_tr - m_tr_ref) <= tol
     for got, key in ((m_all, "val_miou"), (m_sel, "val_miou_selective")):

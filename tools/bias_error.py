@@ -37,7 +37,23 @@ def rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-300))
 
 
+def _heartbeat(period=30.0):
+    """A progress line every `period` seconds (a long silent phase would look hung to the GPU harness)."""
+    import threading
+    import time
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"  ... {time.time() - t0:.0f} s", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    _heartbeat()
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=128)
     ap.add_argument("--size", type=int, default=256)
@@ -122,6 +138,8 @@ def main():
         return z
 
     O._cbr = rec32
+    # torch's native convolutions (im2col + BLAS), not MIOpen: no kernel compilation / search on a fresh box
+    torch.backends.cudnn.enabled = False
     p32, b32 = O.make_state(a.seed, "RGB", selective=True)
     p32 = type(p32)((k, v.detach().to(dev, torch.float32).requires_grad_()) for k, v in p32.items())
     b32 = {k: (v.to(dev, torch.float32) if v.is_floating_point() else v.to(dev)) for k, v in b32.items()}
