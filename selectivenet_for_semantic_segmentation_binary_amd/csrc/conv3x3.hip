@@ -1305,8 +1305,9 @@ constexpr int XTH = 8, XTW = 8, XHW = XTW + 2, XHP = (XTH + 2) * XHW, XPIX = XTH
 // The BN-backward apply fused into the weight gradient's dY staging (selunet_conv3x3_wgrad_x2_bn): P gathers
 // the layer's dA; y, the forward's folded scale / shift (ReLU mask), mean / invstd and the coefficients coef
 // [3][C] of selunet_bn_bwd_stats_finalize form dy = (y sc + sh > 0 ? k0 dA : 0) - k1 - k2 invstd (y - mean)
-// exactly as bn_bwd_apply_kernel; the workgroups of channel chunk 0 write dy (once per element) and the
-// exact max |dy| (atomic max) for the layer's data gradient (WgradBnArg, gemm_common.h).
+// exactly as bn_bwd_apply_kernel; dy is written once per element (pixel px of a tile by the workgroup of
+// channel chunk px % ci_chunks) with its exact max |dy| (atomic max) for the layer's data gradient
+// (WgradBnArg, gemm_common.h).
 template <int BI, bool BNA = false>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_chunks, int64_t tiles_per_split,
@@ -1387,7 +1388,9 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
     Ks[tid] = v;
   }
   float dam = 0.0f;                               // BNA: running max |dy| of this workgroup's stores
-  const bool dy_out = BNA && cik == 0 && bn.dy != nullptr;
+  // BNA: every channel chunk's workgroup forms the whole dY tile; the dy stores are shared out by pixel
+  // (pixel px of a tile is stored by chunk px % ci_chunks), so no chunk's workgroups carry all of them
+  const bool dy_out = BNA && bn.dy != nullptr;
 
   auto tile_origin = [&](int pt, int& img, int& y0, int& x0) __attribute__((always_inline)) {
     const unsigned r2 = (unsigned)pt / (unsigned)tiles_x;
@@ -1469,7 +1472,7 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
         for (int e = 0; e < 4; ++e)
           o[e] = (yv[e] * csc[e] + csh[e] > 0.0f ? ck0[e] * g[e] : 0.0f) - cb[e] - ca[e] * yv[e];
         const float4 d = in ? make_float4(o[0], o[1], o[2], o[3]) : make_float4(0, 0, 0, 0);
-        if (dy_out && in) {
+        if (dy_out && in && px % ci_chunks == cik) {
           const int64_t off = (((int64_t)img * H + y0 + px / XTW) * W + x0 + px % XTW) * pa.C + i0 + cc * 4;
           *reinterpret_cast<float4*>(bn.dy + off) = d;
           dam = fmaxf(dam, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
@@ -1585,8 +1588,8 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   else tile_loop(std::integral_constant<int, 4>{});
 
   if constexpr (BNA) {
-    // the exact max |dy| of the stored dy: one atomic per workgroup of channel chunk 0 (uniform branch)
-    if (cik == 0 && bn.dy_amax) block_amax(bn.dy_amax, dam, Ks);
+    // the exact max |dy| of the stored dy: one atomic per workgroup (uniform branch)
+    if (bn.dy_amax) block_amax(bn.dy_amax, dam, Ks);
   }
   const float ofac = uns_p * uns_x;
   const int ctot = Q.Ctot;
