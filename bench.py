@@ -96,7 +96,8 @@ class KernelTimer:
 
     MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
             "selunet_conv3x3_wx2",
-            "selunet_conv3x3_wgrad_x2", "selunet_conv3x3_wgrad_x2_bn", "selunet_gemm_wgrad_x2",
+            "selunet_conv3x3_wgrad_x2", "selunet_conv3x3_wgrad_x2_bn", "selunet_conv3x3_wgrad_x2_bn_src",
+            "selunet_gemm_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
     HBM = ("selunet_first_conv_fwd", "selunet_first_conv_fwd_centered", "selunet_first_conv_wgrad", "selunet_bn_bwd_apply", "selunet_bn_bwd_apply_amax",
            "selunet_maxpool2_fwd",
@@ -176,6 +177,17 @@ class KernelTimer:
             flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
             nbytes = 3 * self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
             return kname, "mfma_f16", flops, nbytes, f"wgrad x2 bn {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}"
+        if name == "selunet_conv3x3_wgrad_x2_bn_src":  # the pool / heads applies fused (args[10]: the dA source)
+            gp, gq, src = args[0], args[1], args[10]
+            flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)
+            m = gp.n * gp.h * gp.w
+            if src.kind == K.DA_POOL:  # reads y, skip and the pooled gradient, writes dy
+                form, dab = "pool", (1 + (1 if src.skip else 0) + 0.25) * self._src_bytes(gp)
+            else:  # reads y and the heads' gradient planes, writes dy
+                form, dab = "heads", self._src_bytes(gp) + 4.0 * m * src.nh
+            nbytes = dab + self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
+            return (f"conv3x3_wgrad_x2_{form}<64>+reduce", "mfma_f16", flops, nbytes,
+                    f"wgrad x2 {form} {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}")
         if name == "selunet_gemm_wgrad_x2":  # (gp, gq, ws, wsb, layout, out, amax_p0, p1, q0, q1, stream)
             gp, gq = args[0], args[1]
             flops = 3 * 2.0 * gp.n * gp.h * gp.w * self._k(gp) * self._k(gq)  # executed fp16 MFMA work

@@ -119,6 +119,9 @@ typedef struct selunet_bn_bwd_stats {
   const float* mean;   /* batch statistics of the forward pass */
   const float* invstd;
   float* slab;         /* [rows][3][C] */
+  float* amax;         /* nullable: atomic max of |dA| as stored (float bits; zeroed by the caller) — read by
+                        * selunet_maxpool2_bwd and selunet_heads_bwd only, whose sums-only mode never stores
+                        * dA: the range word selunet_bn_bwd_stats_finalize_bound needs for a fused apply */
 } selunet_bn_bwd_stats;
 
 typedef struct selunet_epilogue {
@@ -228,6 +231,28 @@ int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selunet_gather* q
                                 float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
                                 const selunet_bn_bwd_stats* bnb, const float* coef, float* dy, float* dy_amax,
                                 void* stream);
+/* Where selunet_conv3x3_wgrad_x2_bn_src's dY staging takes dA from. TENSOR: p's source (as
+ * selunet_conv3x3_wgrad_x2_bn). POOL: the layer feeds a 2x2 max-pool (model.py:30,60-61's encoder
+ * blocks): dA = route(pooled) + skip, pooled [n][h/2][w/2][C] the pool output's gradient routed to
+ * the first maximum of relu(y*scale+shift) in row-major window order, skip [M][C] (nullable) added to
+ * every pixel — selunet_bn_bwd_apply_pool's dA. HEADS: the layer feeds the 1x1 heads (model.py:62-66):
+ * dA[m][c] = sum_h head_w[h][c] * g[h][m] over nh = 1 or 3 heads, C = 64 — selunet_bn_bwd_apply_heads's
+ * dA. For POOL / HEADS p only gives the grid and C (its data is not read) and C must be 64. */
+enum { SELUNET_DA_TENSOR = 0, SELUNET_DA_POOL = 1, SELUNET_DA_HEADS = 2 };
+typedef struct selunet_da_source {
+  int32_t kind;
+  int32_t nh;
+  const float* pooled;
+  const float* skip;
+  const float* head_w;
+  const float* g[3];
+} selunet_da_source;
+/* selunet_conv3x3_wgrad_x2_bn with dA formed from `src` (NULL: TENSOR): the fused pool / heads applies
+ * (selunet_bn_bwd_apply_pool / _heads) move into the weight gradient's staging like the plain one. */
+int selunet_conv3x3_wgrad_x2_bn_src(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                    float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                                    const selunet_bn_bwd_stats* bnb, const float* coef, const selunet_da_source* src,
+                                    float* dy, float* dy_amax, void* stream);
 int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, int32_t n_cols, int32_t mode, int32_t split);

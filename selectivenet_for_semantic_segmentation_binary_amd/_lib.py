@@ -19,6 +19,7 @@ c_int32, c_int64, c_double, c_float, c_void_p = (ctypes.c_int32, ctypes.c_int64,
 
 F32, BF16 = 0, 1
 EP_PLAIN, EP_SPLIT, EP_SCATTER2X = 0, 1, 2
+DA_TENSOR, DA_POOL, DA_HEADS = 0, 1, 2  # selunet_da_source kinds
 GEMM_BM = 128
 ADAM_CHUNK = 4096
 
@@ -35,7 +36,13 @@ class Gather(ctypes.Structure):
 
 class BnBwdStats(ctypes.Structure):
     _fields_ = [("y", c_void_p), ("scale", c_void_p), ("shift", c_void_p), ("mean", c_void_p),
-                ("invstd", c_void_p), ("slab", c_void_p)]
+                ("invstd", c_void_p), ("slab", c_void_p), ("amax", c_void_p)]
+
+
+class DaSource(ctypes.Structure):
+    """selunet_da_source: where the fused weight gradient's staging forms dA (SELUNET_DA_*)."""
+    _fields_ = [("kind", c_int32), ("nh", c_int32), ("pooled", c_void_p), ("skip", c_void_p), ("head_w", c_void_p),
+                ("g", c_void_p * 3)]
 
 
 class Epilogue(ctypes.Structure):
@@ -106,6 +113,9 @@ SIGNATURES = {
                                            P]),
     "selunet_conv3x3_wgrad_x2_bn": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int64, P, P, P, P,
                                               ctypes.POINTER(BnBwdStats), P, P, P, P]),
+    "selunet_conv3x3_wgrad_x2_bn_src": (c_int32, [ctypes.POINTER(Gather), ctypes.POINTER(Gather), P, c_int64, P, P, P,
+                                                  P, ctypes.POINTER(BnBwdStats), P, ctypes.POINTER(DaSource), P, P,
+                                                  P]),
     "selunet_gemm_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32, c_int32]),
     "selunet_gemm_gather_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
     "selunet_set_halo_workgroups": (c_int32, [c_int32]),

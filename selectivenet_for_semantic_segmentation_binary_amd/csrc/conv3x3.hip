@@ -1307,8 +1307,10 @@ constexpr int XTH = 8, XTW = 8, XHW = XTW + 2, XHP = (XTH + 2) * XHW, XPIX = XTH
 // [3][C] of selunet_bn_bwd_stats_finalize form dy = (y sc + sh > 0 ? k0 dA : 0) - k1 - k2 invstd (y - mean)
 // exactly as bn_bwd_apply_kernel; dy is written once per element (pixel px of a tile by the workgroup of
 // channel chunk px % ci_chunks) with its exact max |dy| (atomic max) for the layer's data gradient
-// (WgradBnArg, gemm_common.h).
-template <int BI, bool BNA = false>
+// (WgradBnArg, gemm_common.h). BNA: 0 no apply; 1 dA from P; 2 dA = route(pooled) + skip of a max-pooled
+// layer (bn_bwd_apply_pool_kernel's dA: the first maximum of relu(y sc + sh) in row-major window order);
+// 3 dA = sum_h w_h g_h of the 1x1 heads (bn_bwd_apply_heads_kernel's). Modes 2 and 3 are BI = 64 only.
+template <int BI, int BNA = 0>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_chunks, int64_t tiles_per_split,
                         int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
@@ -1320,8 +1322,12 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   constexpr int NTAP = TG == 1 ? 9 : 5;          // accumulators per wave
   constexpr int P_ROUNDS = (XPIX * BI / 4) / 512;
   constexpr int X_ROUNDS = (XHP * 16 + 511) / 512;
-  constexpr int KX = BNA ? 5 * BI : 2 * BI;      // coefficient area: dY side (sc, sh[, k0, a, b]), then the halo's
+  constexpr bool POOL = BNA == 2, HEADS = BNA == 3;
+  // coefficient area: dY side (sc, sh[, k0, a, b[, w0, w1, w2]]), then the halo's
+  constexpr int KX = BNA ? (HEADS ? 8 : 5) * BI : 2 * BI;
+  constexpr int NWIN = XPIX * BI / 16;            // POOL: 2x2 windows x 4 channels of a dY tile, one per thread
   static_assert(P_ROUNDS * 512 == XPIX * BI / 4, "dY tile must split evenly over the threads");
+  static_assert(!(POOL || HEADS) || (BI == 64 && NWIN <= 512), "pool / heads sources are BI = 64 forms");
 
   __shared__ __attribute__((aligned(16))) _Float16 Ps[2][2][XPIX][LDP];  // [buffer][h, l][pixel][co]
   __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][XHP][LDX];   // [buffer][h, l][halo pixel][ci]
@@ -1368,7 +1374,11 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
         case 1: v = bn.shift[c]; break;
         case 2: v = bn.coef[c]; break;                                       // k0
         case 3: v = bn.coef[2 * C + c] * bn.invstd[c]; break;                // a = k2 invstd
-        default: v = bn.coef[C + c] - bn.coef[2 * C + c] * bn.invstd[c] * bn.mean[c];  // b = k1 - a mean
+        case 4: v = bn.coef[C + c] - bn.coef[2 * C + c] * bn.invstd[c] * bn.mean[c]; break;  // b = k1 - a mean
+        default: {                                                            // HEADS: w_h[c]
+          const int hd = k / BI - 5;
+          v = hd < bn.nh ? bn.hw[hd * 64 + c] : 0.0f;
+        }
       }
       Ks[k] = v;
     }
@@ -1421,19 +1431,44 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   };
   float4 rp[P_ROUNDS], rx[X_ROUNDS];
   float4 ry[BNA ? P_ROUNDS : 1];                  // BNA: y at the dA elements
+  float rg[HEADS ? P_ROUNDS : 1][3];              // HEADS: the heads' gradients at the pixel
+  float4 wy[POOL ? 4 : 1], wk[POOL ? 4 : 1], wg;  // POOL: y and skip at a window's 4 pixels, the pooled gradient
   // rounds [r0, r1) of the dY tile (BNA at BI = 128 stages it in two halves: dA and y of half a tile live
   // at a time, as many registers as the plain kernel's whole dY tile)
   auto load_p = [&](int pt, int r0, int r1) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
+    if constexpr (POOL) {  // window wi = tid / (BI / 4) of the tile, channels (tid % (BI / 4)) * 4
+      if (r0 == 0 && tid < NWIN) {
+        const int wi = tid / (BI / 4), cg = tid % (BI / 4);
+        const int yy = min(y0 + 2 * (wi / (XTW / 2)), H - 2), xx = min(x0 + 2 * (wi % (XTW / 2)), W - 2);
+        const int64_t b0 = (((int64_t)img * H + yy) * W + xx) * pa.C + i0 + cg * 4, rs = (int64_t)W * pa.C;
+        const int64_t off[4] = {b0, b0 + pa.C, b0 + rs, b0 + rs + pa.C};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          wy[k] = *reinterpret_cast<const float4*>(bn.y + off[k]);
+          wk[k] = bn.skip ? *reinterpret_cast<const float4*>(bn.skip + off[k]) : make_float4(0, 0, 0, 0);
+        }
+        wg = *reinterpret_cast<const float4*>(
+            bn.pooled + (((int64_t)img * (H / 2) + yy / 2) * (W / 2) + xx / 2) * pa.C + i0 + cg * 4);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
       if (r < r0 || r >= r1) continue;
       const int idx = r * 512 + tid;
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const int y = min(y0 + px / XTW, H - 1), x = min(x0 + px % XTW, W - 1);
-      const int64_t off = (((int64_t)img * H + y) * W + x) * pa.C + i0 + cc * 4;
-      rp[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pa.data) + off);
+      const int64_t pix = ((int64_t)img * H + y) * W + x;
+      const int64_t off = pix * pa.C + i0 + cc * 4;
+      if constexpr (HEADS) {
+        rg[r][0] = bn.g0[pix];
+        rg[r][1] = bn.nh > 1 ? bn.g1[pix] : 0.0f;
+        rg[r][2] = bn.nh > 1 ? bn.g2[pix] : 0.0f;
+      } else {
+        rp[r] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pa.data) + off);
+      }
       if constexpr (BNA) ry[r] = *reinterpret_cast<const float4*>(bn.y + off);
     }
   };
@@ -1452,6 +1487,53 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   auto store_p = [&](int pt, int buf, int r0, int r1) __attribute__((always_inline)) {
     int img, y0, x0;
     tile_origin(pt, img, y0, x0);
+    if constexpr (POOL) {
+      if (r0 == 0 && tid < NWIN) {
+        const int wi = tid / (BI / 4), cg = tid % (BI / 4);
+        const int wyy = 2 * (wi / (XTW / 2)), wxx = 2 * (wi % (XTW / 2));
+        const bool in = y0 + wyy < H && x0 + wxx < W;  // (H, W even: a window is wholly in or out)
+        const f32x4 csc = *reinterpret_cast<const f32x4*>(Ks + cg * 4);
+        const f32x4 csh = *reinterpret_cast<const f32x4*>(Ks + BI + cg * 4);
+        const f32x4 ck0 = *reinterpret_cast<const f32x4*>(Ks + 2 * BI + cg * 4);
+        const f32x4 ca = *reinterpret_cast<const f32x4*>(Ks + 3 * BI + cg * 4);
+        const f32x4 cb = *reinterpret_cast<const f32x4*>(Ks + 4 * BI + cg * 4);
+        const float yv[4][4] = {{wy[0].x, wy[0].y, wy[0].z, wy[0].w}, {wy[1].x, wy[1].y, wy[1].z, wy[1].w},
+                                {wy[2].x, wy[2].y, wy[2].z, wy[2].w}, {wy[3].x, wy[3].y, wy[3].z, wy[3].w}};
+        const float gv[4] = {wg.x, wg.y, wg.z, wg.w};
+        int arg[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float best = fmaxf(yv[0][e] * csc[e] + csh[e], 0.0f);
+#pragma unroll
+          for (int k = 1; k < 4; ++k) {
+            const float v = fmaxf(yv[k][e] * csc[e] + csh[e], 0.0f);
+            if (v > best) {  // first maximum in row-major window order (strict >), as bn_bwd_apply_pool_kernel
+              best = v;
+              arg[e] = k;
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float d[4] = {wk[k].x, wk[k].y, wk[k].z, wk[k].w};
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (arg[e] == k) d[e] += gv[e];
+            o[e] = (yv[k][e] * csc[e] + csh[e] > 0.0f ? ck0[e] * d[e] : 0.0f) - cb[e] - ca[e] * yv[k][e];
+          }
+          const int py = wyy + (k >> 1), pxx = wxx + (k & 1), px = py * XTW + pxx;
+          const float4 dv = in ? make_float4(o[0], o[1], o[2], o[3]) : make_float4(0, 0, 0, 0);
+          if (dy_out && in && px % ci_chunks == cik) {
+            const int64_t off = (((int64_t)img * H + y0 + py) * W + x0 + pxx) * pa.C + i0 + cg * 4;
+            *reinterpret_cast<float4*>(bn.dy + off) = dv;
+            dam = fmaxf(dam, fmaxf(fmaxf(fabsf(dv.x), fabsf(dv.y)), fmaxf(fabsf(dv.z), fabsf(dv.w))));
+          }
+          put(dv, nullptr, nullptr, 0, sp, &Ps[buf][0][px][cg * 4], &Ps[buf][1][px][cg * 4]);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < P_ROUNDS; ++r) {
       if (r < r0 || r >= r1) continue;
@@ -1459,8 +1541,16 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
       const int px = idx / (BI / 4), cc = idx % (BI / 4);
       const bool in = y0 + px / XTW < H && x0 + px % XTW < W;
       if constexpr (BNA) {
-        // dy of 4 channels (bn_bwd_apply_kernel's arithmetic), written once by channel chunk 0
-        const float g[4] = {rp[r].x, rp[r].y, rp[r].z, rp[r].w}, yv[4] = {ry[r].x, ry[r].y, ry[r].z, ry[r].w};
+        // dy of 4 channels (bn_bwd_apply_kernel's arithmetic)
+        float g[4] = {rp[r].x, rp[r].y, rp[r].z, rp[r].w};
+        const float yv[4] = {ry[r].x, ry[r].y, ry[r].z, ry[r].w};
+        if constexpr (HEADS) {  // dA = w0 g0 + w1 g1 + w2 g2 (bn_bwd_apply_heads_kernel's form)
+          const f32x4 w0 = *reinterpret_cast<const f32x4*>(Ks + 5 * BI + cc * 4);
+          const f32x4 w1 = *reinterpret_cast<const f32x4*>(Ks + 6 * BI + cc * 4);
+          const f32x4 w2 = *reinterpret_cast<const f32x4*>(Ks + 7 * BI + cc * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g[e] = w0[e] * rg[r][0] + w1[e] * rg[r][1] + w2[e] * rg[r][2];
+        }
         // the 4 channels' coefficients: one 16-B LDS read per coefficient row
         const f32x4 csc = *reinterpret_cast<const f32x4*>(Ks + cc * 4);
         const f32x4 csh = *reinterpret_cast<const f32x4*>(Ks + BI + cc * 4);
@@ -2150,8 +2240,12 @@ int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, i
   int64_t per;
   const int64_t splits = conv3x3_wgrad_x2_splits(p, q, &per);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
-  auto k = bi == 128 ? (bn ? conv3x3_wgrad_x2_kernel<128, true> : conv3x3_wgrad_x2_kernel<128, false>)
-                     : (bn ? conv3x3_wgrad_x2_kernel<64, true> : conv3x3_wgrad_x2_kernel<64, false>);
+  const int kind = bn ? bn->kind : -1;
+  SELUNET_REQUIRE(kind <= SELUNET_DA_TENSOR || bi == 64, "conv3x3_wgrad_x2: pool / heads dA sources need 64 columns");
+  auto k = bi == 128 ? (bn ? conv3x3_wgrad_x2_kernel<128, 1> : conv3x3_wgrad_x2_kernel<128, 0>)
+           : kind == SELUNET_DA_POOL  ? conv3x3_wgrad_x2_kernel<64, 2>
+           : kind == SELUNET_DA_HEADS ? conv3x3_wgrad_x2_kernel<64, 3>
+           : (bn ? conv3x3_wgrad_x2_kernel<64, 1> : conv3x3_wgrad_x2_kernel<64, 0>);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(512), 0, st, p, q, ldo, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
                      ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1, bn ? *bn : WgradBnArg{});
   return check_launch("conv3x3_wgrad_x2");

@@ -1564,10 +1564,10 @@ extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_g
   return check_launch("conv3x3_wgrad_x2");
 }
 
-extern "C" int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
-                                           float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
-                                           const selunet_bn_bwd_stats* bnb, const float* coef, float* dy, float* dy_amax,
-                                           void* stream) {
+extern "C" int selunet_conv3x3_wgrad_x2_bn_src(const selunet_gather* p, const selunet_gather* q, float* ws,
+                                               int64_t ws_bytes, float* out, const float* amax_p, const float* amax_q0,
+                                               const float* amax_q1, const selunet_bn_bwd_stats* bnb, const float* coef,
+                                               const selunet_da_source* src, float* dy, float* dy_amax, void* stream) {
   WgradPlan w;
   if (int rc = plan_wgrad_x2(p, q, w)) return rc;
   const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
@@ -1579,10 +1579,33 @@ extern "C" int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selune
                   "conv3x3_wgrad_x2_bn: y, scale, shift, mean, invstd and coef are required");
   SELUNET_REQUIRE(p->nsrc == 1 && p->src[0].scale == nullptr && p->src[0].layout == 0,
                   "conv3x3_wgrad_x2_bn: p gathers dA alone (one source, no transform)");
-  SELUNET_REQUIRE(dy == nullptr || (dy != p->src[0].data && dy != bnb->y), "conv3x3_wgrad_x2_bn: dy must not alias dA or y");
   SELUNET_REQUIRE((dy == nullptr) == (dy_amax == nullptr), "conv3x3_wgrad_x2_bn: dy and dy_amax go together");
-  const WgradBnArg bn{reinterpret_cast<const float*>(bnb->y), bnb->scale, bnb->shift, bnb->mean, bnb->invstd, coef, dy,
-                      dy_amax};
+  WgradBnArg bn{reinterpret_cast<const float*>(bnb->y), bnb->scale, bnb->shift, bnb->mean, bnb->invstd, coef, dy,
+                dy_amax, SELUNET_DA_TENSOR, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const int kind = src ? src->kind : SELUNET_DA_TENSOR;
+  if (kind == SELUNET_DA_TENSOR) {
+    SELUNET_REQUIRE(dy == nullptr || (dy != p->src[0].data && dy != bnb->y), "conv3x3_wgrad_x2_bn: dy must not alias dA or y");
+  } else if (kind == SELUNET_DA_POOL) {
+    SELUNET_REQUIRE(w.gp.K == 64 && w.gp.h % 2 == 0 && w.gp.w % 2 == 0 && src->pooled != nullptr,
+                    "conv3x3_wgrad_x2_bn: a pool source needs C = 64, an even grid and the pooled gradient");
+    SELUNET_REQUIRE(dy == nullptr || (dy != src->pooled && dy != src->skip && dy != bnb->y),
+                    "conv3x3_wgrad_x2_bn: dy must not alias y, the pooled or the skip gradient");
+    bn.pooled = src->pooled;
+    bn.skip = src->skip;
+  } else if (kind == SELUNET_DA_HEADS) {
+    SELUNET_REQUIRE(w.gp.K == 64 && (src->nh == 1 || src->nh == 3) && src->head_w && src->g[0] &&
+                        (src->nh == 1 || (src->g[1] && src->g[2])),
+                    "conv3x3_wgrad_x2_bn: a heads source needs C = 64, nh = 1 or 3, the head weights and planes");
+    SELUNET_REQUIRE(dy == nullptr || dy != bnb->y, "conv3x3_wgrad_x2_bn: dy must not alias y");
+    bn.nh = src->nh;
+    bn.hw = src->head_w;
+    bn.g0 = src->g[0];
+    bn.g1 = src->g[1];
+    bn.g2 = src->g[2];
+  } else {
+    return fail(SELUNET_EINVAL, "conv3x3_wgrad_x2_bn: unknown dA source kind %d", kind);
+  }
+  bn.kind = kind;
   hipStream_t st = as_stream(stream);
   if (int rc = conv3x3_wgrad_x2_launch(w.gp, w.gq, ws, w.nj_pad, amax_p, amax_q0, amax_q1, st, &bn)) return rc;
   const int64_t n4 = (int64_t)w.ni * w.nj_pad / 4;
@@ -1590,6 +1613,14 @@ extern "C" int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selune
   hipLaunchKernelGGL(wgrad_reduce_kernel<WG_CONV3X3>, dim3(blocks), dim3(64), 0, st, ws, w.splits,
                      (int64_t)w.ni * w.nj_pad, w.ni, w.nj_pad, w.gq.K, out);
   return check_launch("conv3x3_wgrad_x2_bn");
+}
+
+extern "C" int selunet_conv3x3_wgrad_x2_bn(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
+                                           float* out, const float* amax_p, const float* amax_q0, const float* amax_q1,
+                                           const selunet_bn_bwd_stats* bnb, const float* coef, float* dy, float* dy_amax,
+                                           void* stream) {
+  return selunet_conv3x3_wgrad_x2_bn_src(p, q, ws, ws_bytes, out, amax_p, amax_q0, amax_q1, bnb, coef, nullptr, dy,
+                                         dy_amax, stream);
 }
 
 // generic fp32 weight gradient on split-fp16 operands (gemm_wgrad_x2_kernel + the fixed-order split

@@ -499,6 +499,14 @@ struct WgradBnArg {
   const float* coef;
   float* dy;
   float* dy_amax;
+  int kind;             // SELUNET_DA_*: where dA comes from (selunet_da_source)
+  int nh;               // HEADS: 1 or 3
+  const float* pooled;  // POOL: [n][h/2][w/2][C]
+  const float* skip;    // POOL: nullable [M][C]
+  const float* hw;      // HEADS: [nh][64]
+  const float* g0;      // HEADS: [M] planes
+  const float* g1;
+  const float* g2;
 };
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
                             const float* amax_q0, const float* amax_q1, hipStream_t st,

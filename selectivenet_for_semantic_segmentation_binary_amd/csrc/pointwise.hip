@@ -839,7 +839,8 @@ struct BnbAcc {
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w, int C, const float* scale,
                                    const float* shift, const T* __restrict__ dp, const T* __restrict__ dskip,
-                                   T* __restrict__ dz, const float* mean, const float* invstd, float* bn_slab) {
+                                   T* __restrict__ dz, const float* mean, const float* invstd, float* bn_slab,
+                                   float* da_amax) {
   const int ho = h >> 1, wo = w >> 1;
   const int CG = C >> 2;
   const int64_t nv = (int64_t)n * ho * wo * CG;
@@ -852,6 +853,7 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
     is = *reinterpret_cast<const f32x4*>(invstd + c);
   }
   BnbAcc bn;
+  float am = 0.0f;  // da_amax: max |dA| as stored
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned p = (unsigned)(i / CG);  // output pixel (< 2^31: checked on the host)
     const unsigned xo = p % (unsigned)wo, t = p / (unsigned)wo;
@@ -882,14 +884,18 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ y, int n, int h, int w,
       for (int e = 0; e < 4; ++e)
         if (arg[e] == q) o[e] += g[e];
       if (dz) Vec4<T>::store(dz + off[q], o);  // (null: the sums only, selunet_bn_bwd_apply_pool forms dz)
-      if (bn_slab) {
+      if (bn_slab || da_amax) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = to_f(from_f<T>(o[e]));  // as stored
-        bn.add(yr[q], o, sc, sh, mu, is);
+        if (bn_slab) bn.add(yr[q], o, sc, sh, mu, is);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(o[e]));
       }
     }
   }
   if (bn_slab) channel_block_reduce<3>(bn.acc, C, bn_slab + (int64_t)blockIdx.x * 3 * C);
+  __shared__ float wred[TPB / 64];
+  if (da_amax) block_amax(da_amax, am, wred);
 }
 
 // =========================================================================== 1x1 heads (C = 64)
@@ -950,7 +956,8 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
                                  const float* __restrict__ shift, const float* __restrict__ w, int nh,
                                  const float* __restrict__ g0, const float* __restrict__ g1,
                                  const float* __restrict__ g2, T* __restrict__ dz, float* slab,
-                                 const float* __restrict__ mean, const float* __restrict__ invstd, float* bn_slab) {
+                                 const float* __restrict__ mean, const float* __restrict__ invstd, float* bn_slab,
+                                 float* da_amax) {
   const int sub = threadIdx.x & 15;
   const int c = sub * 4;
   const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
@@ -965,6 +972,7 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     is = *reinterpret_cast<const f32x4*>(invstd + c);
   }
   BnbAcc bn;
+  float am = 0.0f;  // da_amax: max |dA| as stored
   const int64_t rows = gridDim.x;
   const int64_t chunk = (m + rows - 1) / rows;
   const int64_t p0 = blockIdx.x * chunk, p1 = std::min<int64_t>(m, p0 + chunk);
@@ -974,10 +982,12 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     for (int e = 0; e < 4; ++e) z[e] = fmaxf(yv[e] * sc[e] + sh[e], 0.0f);
     f32x4 d = wv[0] * g[0] + wv[1] * g[1] + wv[2] * g[2];  // (as bn_bwd_apply_heads_kernel forms it)
     if (dz) Vec4<T>::store(dz + p * 64 + c, d);  // (null: the sums only, selunet_bn_bwd_apply_heads forms dz)
-    if (bn_slab) {
+    if (bn_slab || da_amax) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[e] = to_f(from_f<T>(d[e]));  // as stored
-      bn.add(yv, d, sc, sh, mu, is);
+      if (bn_slab) bn.add(yv, d, sc, sh, mu, is);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(d[e]));
     }
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
@@ -1036,6 +1046,8 @@ __global__ void heads_bwd_kernel(const T* __restrict__ y, int64_t m, const float
     __syncthreads();
   }
   if (bn_slab) channel_block_reduce<3>(bn.acc, 64, bn_slab + (int64_t)blockIdx.x * 3 * 64);
+  __shared__ float wred[TPB / 64];
+  if (da_amax) block_amax(da_amax, am, wred);
 }
 
 // =========================================================================== BN-backward apply with dA formed
@@ -2000,7 +2012,8 @@ int selunet_maxpool2_bwd(const void* y, int32_t n, int32_t h, int32_t w, int32_t
   }
   DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3((unsigned)selunet_maxpool2_bwd_slab_rows(n, h, w, c)),
                                        dim3(TPB), 0, as_stream(stream), (const T*)y, n, h, w, c, scale, shift,
-                                       (const T*)dpool, (const T*)dskip, (T*)dz, mean, invstd, bslab));
+                                       (const T*)dpool, (const T*)dskip, (T*)dz, mean, invstd, bslab,
+                                       bnb ? bnb->amax : nullptr));
   return check_launch("maxpool2_bwd");
 }
 
@@ -2030,7 +2043,7 @@ int selunet_heads_bwd(const void* y, int64_t m, const float* scale, const float*
   }
   DISPATCH_T(dtype, hipLaunchKernelGGL(heads_bwd_kernel<T>, dim3((unsigned)channel_slab_rows(m)), dim3(TPB), 0,
                                        as_stream(stream), (const T*)y, m, scale, shift, w, nh, g0, g1, g2, (T*)dz,
-                                       slab, mean, invstd, bslab));
+                                       slab, mean, invstd, bslab, bnb ? bnb->amax : nullptr));
   return check_launch("heads_bwd");
 }
 

@@ -13,6 +13,7 @@ bottleneck -> pool3 backward (+ d(skip3)) -> enc3_2 -> ... -> enc1_1 (no data gr
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import weakref
 from collections import OrderedDict
@@ -92,10 +93,13 @@ class DGrad:
     rows: int = 0
     apply: object = None
     da_word: bool = False  # the producer recorded max |t| in ctx.words["da:" + layer] (fused apply's bound)
+    src: object = None  # K.DaSource: dA of a sums-only producer (pool / heads) the fused weight gradient forms
 
 
-def bnb_for(st: BNState, slab) -> K.BnBwdStats:
-    return K.BnBwdStats(K.ptr(st.y), K.ptr(st.scale), K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(slab))
+def bnb_for(st: BNState, slab, amax=None) -> K.BnBwdStats:
+    """amax (nullable): the word a sums-only pool / heads producer records max |dA| into."""
+    return K.BnBwdStats(K.ptr(st.y), K.ptr(st.scale), K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(slab),
+                        K.ptr(amax))
 
 
 @dataclass
@@ -158,6 +162,9 @@ class Engine:
         # split-fp16 training: the BN-backward apply of layers whose dA is stored runs inside their weight
         # gradient (selunet_conv3x3_wgrad_x2_bn); SELUNET_FUSE_WGRAD_APPLY=0 keeps the separate apply
         self.fuse_wgrad_apply = os.environ.get("SELUNET_FUSE_WGRAD_APPLY", "1") != "0"
+        # ... and for the 64-channel layers whose dA is formed on the fly (encoder_layer_1_2 from the pool's
+        # gradient, decoder_layer_1_1 from the heads'): SELUNET_FUSE_WGRAD_SRC=0 keeps their separate applies
+        self.fuse_wgrad_src = os.environ.get("SELUNET_FUSE_WGRAD_SRC", "1") != "0"
         self._plans = OrderedDict()  # signature -> [_Entry]
 
     # ------------------------------------------------------------------ small helpers
@@ -603,11 +610,14 @@ class Engine:
         # the BN-backward apply fused into the split-fp16 weight gradient: dA's producer
         # recorded max |dA|, the finalize turns it into a bound of |dy|, the weight gradient forms dy from
         # (dA, y) while staging and writes it (with its exact max) for the data gradient
-        fuse = (wp is not None and wp.mode in X2_MODES and dg.apply is None and dg.t is not None and dg.da_word and
-                self.fuse_wgrad_apply and all(sr.amax is not None for sr in input_srcs))
+        # (a sums-only producer's dA, dg.src, at 64 channels: the pool / heads forms of the staging)
+        src = dg.src if (dg.src is not None and co == 64 and self.fuse_wgrad_src) else None
+        fuse = (wp is not None and wp.mode in X2_MODES and dg.da_word and self.fuse_wgrad_apply and
+                (src is not None or (dg.apply is None and dg.t is not None)) and
+                all(sr.amax is not None for sr in input_srcs))
         gp = gq = None
-        if fuse:
-            gp = K.gather(st.n, st.h, st.w, 1, K.source(dg.t, co))
+        if fuse:  # (with a src, p only gives the grid and channel count: y stands in for dA)
+            gp = K.gather(st.n, st.h, st.w, 1, K.source(dg.t if src is None else st.y, co))
             gq = K.gather(st.n, st.h, st.w, q_taps, *input_srcs)
             fuse = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq) > 0
         if fuse:
@@ -641,9 +651,12 @@ class Engine:
             wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq)
             wsx = K.keep(torch.empty(wsb // 4, dtype=torch.float32, device=dev))
             words = [sr.amax for sr in input_srcs]
-            K.call("selunet_conv3x3_wgrad_x2_bn", gp, gq, K.ptr(wsx), wsb, K.ptr(G[f"{name}.0.weight"]),
-                   K.ptr(self._word(ctx, "dyb:" + name)), K.ptr(words[0]), K.ptr(words[1]) if len(words) > 1 else None,
-                   bnb_for(st, None), K.ptr(coef), K.ptr(dy), K.ptr(dyw), self.stream)
+            args = (gp, gq, K.ptr(wsx), wsb, K.ptr(G[f"{name}.0.weight"]), K.ptr(self._word(ctx, "dyb:" + name)),
+                    K.ptr(words[0]), K.ptr(words[1]) if len(words) > 1 else None, bnb_for(st, None), K.ptr(coef))
+            if src is not None:
+                K.call("selunet_conv3x3_wgrad_x2_bn_src", *args, src, K.ptr(dy), K.ptr(dyw), self.stream)
+            else:
+                K.call("selunet_conv3x3_wgrad_x2_bn", *args, K.ptr(dy), K.ptr(dyw), self.stream)
         else:
             if dg.apply is not None:  # dA formed on the fly from its producer's inputs
                 dg.apply(dy, coef, dyw)
@@ -726,19 +739,21 @@ class Engine:
             K.call("selunet_gemm_gather", ga, K.ptr(wd), ci, 4 * co, ep, self.code, self.stream)
         return DGrad(dz, slab, rows, da_word=da_word)
 
-    def _pool_bwd(self, st: BNState, dp: DGrad, dskip):
+    def _pool_bwd(self, ctx, st: BNState, dp: DGrad, dskip):
         rows = K.query("selunet_maxpool2_bwd_slab_rows", st.n, st.h, st.w, st.c)
         slab = K.keep(torch.empty(rows, 3, st.c, dtype=torch.float32, device=st.y.device))
-        bnb = bnb_for(st, slab)
         if K.fused_apply_enabled():  # the sums only; the layer's BN-backward apply routes dP itself
+            word = ctx.words.get("da:" + st.name) if ctx.x2 else None  # max |dA| for the fused weight gradient
             K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
-                   K.ptr(dp.t), K.ptr(dskip), None, bnb, self.code, self.stream)
+                   K.ptr(dp.t), K.ptr(dskip), None, bnb_for(st, slab, word), self.code, self.stream)
 
             def apply(dy, coef, word):
                 K.call("selunet_bn_bwd_apply_pool", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale),
                        K.ptr(st.shift), K.ptr(st.mean), K.ptr(st.invstd), K.ptr(coef), K.ptr(dp.t), K.ptr(dskip),
                        K.ptr(dy), K.ptr(word), self.code, self.stream)
-            return DGrad(None, slab, rows, apply)
+            src = K.DaSource(K.DA_POOL, 0, K.ptr(dp.t), K.ptr(dskip))
+            return DGrad(None, slab, rows, apply, da_word=word is not None, src=src)
+        bnb = bnb_for(st, slab)
         dz = K.keep(torch.empty_like(st.y))
         K.call("selunet_maxpool2_bwd", K.ptr(st.y), st.n, st.h, st.w, st.c, K.ptr(st.scale), K.ptr(st.shift),
                K.ptr(dp.t), K.ptr(dskip), K.ptr(dz), bnb, self.code, self.stream)
@@ -807,11 +822,14 @@ class Engine:
             slab = K.keep(torch.empty(rows, nh * 65, dtype=torch.float32, device=dev))
             fused = K.fused_apply_enabled()  # sums only: decoder_layer_1_1's apply forms dA from the g planes
             dz = None if fused else K.keep(torch.empty(M, 64, dtype=self.dt, device=dev))
+            # max |dA| for the fused weight gradient (sums-only mode)
+            hword = ctx.words.get("da:decoder_layer_1_1") if (ctx.x2 and fused) else None
             K.call("selunet_heads_bwd", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift), K.ptr(ctx.head_w), nh,
-                   K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab), self.code,
-                   self.stream)
+                   K.ptr(gs[0]), K.ptr(gs[1]), K.ptr(gs[2]), K.ptr(dz), K.ptr(slab), bnb_for(d11, bslab, hword),
+                   self.code, self.stream)
             seg = nh * 65
         apply = apply_planes if (ce is not None and dz is None) else None
+        hsrc = None
         if dz is None and ce is None:
             head_w = ctx.head_w
 
@@ -819,7 +837,9 @@ class Engine:
                 K.call("selunet_bn_bwd_apply_heads", K.ptr(d11.y), M, K.ptr(d11.scale), K.ptr(d11.shift),
                        K.ptr(d11.mean), K.ptr(d11.invstd), K.ptr(coef), K.ptr(head_w), nh, K.ptr(gs[0]), K.ptr(gs[1]),
                        K.ptr(gs[2]), K.ptr(dy), K.ptr(word), self.code, self.stream)
-        dz = DGrad(dz, bslab, rows, apply)
+            g3 = (ctypes.c_void_p * 3)(*[K.ptr(g) for g in gs[:3]])
+            hsrc = K.DaSource(K.DA_HEADS, nh, None, None, K.ptr(head_w), g3)
+        dz = DGrad(dz, bslab, rows, apply, da_word=hsrc is not None and hword is not None, src=hsrc)
         # the head weight/bias grads are one consecutive segment of the gradient buffer (registration
         # order conv1x1, conv_select, conv_aux; weight then bias each): reduce straight into it
         hw0 = G[f"{heads[0]}.weight"]
@@ -853,12 +873,12 @@ class Engine:
         dz = self._up_bwd(ctx, "unpool3", du3, G, bn["decoder_layer_4_1"])
         dz = cb("decoder_layer_4_1", dz, [bn["decoder_layer_4_2"].src()], prev=bn["decoder_layer_4_2"])
         dp3 = cb("decoder_layer_4_2", dz, [K.source(p3, 256, amax=e32.amax)])
-        dz = self._pool_bwd(e32, dp3, dskip3)
+        dz = self._pool_bwd(ctx, e32, dp3, dskip3)
         dz = cb("encoder_layer_3_2", dz, [bn["encoder_layer_3_1"].src()], prev=bn["encoder_layer_3_1"])
         dp2 = cb("encoder_layer_3_1", dz, [K.source(p2, 128, amax=e22.amax)])
-        dz = self._pool_bwd(e22, dp2, dskip2)
+        dz = self._pool_bwd(ctx, e22, dp2, dskip2)
         dz = cb("encoder_layer_2_2", dz, [bn["encoder_layer_2_1"].src()], prev=bn["encoder_layer_2_1"])
         dp1 = cb("encoder_layer_2_1", dz, [K.source(p1, 64, amax=e12.amax)])
-        dz = self._pool_bwd(e12, dp1, dskip1)
+        dz = self._pool_bwd(ctx, e12, dp1, dskip1)
         dz = cb("encoder_layer_1_2", dz, [bn["encoder_layer_1_1"].src()], prev=bn["encoder_layer_1_1"])
         cb("encoder_layer_1_1", dz, [], need_dgrad=False, first_x=ctx.x)

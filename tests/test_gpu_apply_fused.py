@@ -3,6 +3,8 @@ unfused pair it replaces: the producer writing dA (selunet_heads_bwd / selunet_m
 selunet_bn_bwd_apply_amax reading it. The producers' sums-only mode (dz = NULL) must write the same
 BN-backward and head-weight sums, and the fused apply the same dy and range word, bit for bit (same
 arithmetic, dA rounded to the tensor dtype as stored) — in fp32 and bf16."""
+import ctypes
+
 import pytest
 import torch
 
@@ -268,3 +270,133 @@ def test_wgrad_x2_bn_equals_apply_then_wgrad(co, ci):
     print(f"wgrad rel err unfused {e0:.2e} fused {e1:.2e}")
     assert e1 < 2e-6 and e0 < 2e-6
     assert rel(dw1.cpu(), dw0.cpu().double()) < 2e-6
+
+
+@pytest.mark.parametrize("form", ["pool", "pool_noskip", "heads1", "heads3"])
+def test_sums_only_producers_record_max_da(form):
+    """selunet_maxpool2_bwd / selunet_heads_bwd in sums-only mode with bnb.amax: the word is max |dA| of the
+    dA the storing mode writes, bit for bit (the bound selunet_bn_bwd_stats_finalize_bound starts from)."""
+    n, h, w, c = 2, 18, 36, 64
+    m = n * h * w
+    y = ((gen(m, c, seed=91) * 2).round() / 2).to(DEV)
+    sc, sh, mean, invstd, _ = coefs(c, 92)
+    res = []
+    for fused in (False, True):
+        rows = (K.query("selunet_maxpool2_bwd_slab_rows", n, h, w, c) if form.startswith("pool")
+                else K.query("selunet_channel_slab_rows", m))
+        bslab = torch.empty(rows, 3, c, device=DEV)
+        word = torch.zeros(1, device=DEV)
+        bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(bslab),
+                           K.ptr(word) if fused else None)
+        dz = None if fused else torch.empty(m, c, device=DEV)
+        if form.startswith("pool"):
+            dp = (gen(m // 4, c, seed=93) * 1e-2).to(DEV)
+            ds = (gen(m, c, seed=94) * 1e-2).to(DEV) if form == "pool" else None
+            K.call("selunet_maxpool2_bwd", K.ptr(y), n, h, w, c, K.ptr(sc), K.ptr(sh), K.ptr(dp), K.ptr(ds), K.ptr(dz),
+                   bnb, K.F32, K.stream_ptr())
+        else:
+            nh = int(form[-1])
+            wt = (gen(3, 64, seed=95) * 0.2).to(DEV).contiguous()
+            g = [(gen(m, seed=96 + i) * 1e-3).to(DEV) for i in range(3)]
+            slab = torch.empty(K.query("selunet_channel_slab_rows", m), nh * 65, device=DEV)
+            K.call("selunet_heads_bwd", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(wt), nh,
+                   *[K.ptr(g[i]) if i < nh else None for i in range(3)], K.ptr(dz), K.ptr(slab), bnb, K.F32,
+                   K.stream_ptr())
+        torch.cuda.synchronize()
+        res.append((dz, word.item(), bslab.cpu()))
+    (dz, _, b0), (_, wd, b1) = res
+    assert torch.equal(b0, b1)
+    assert wd == dz.abs().max().item() > 0
+
+
+def _src_case(form, seed=100):
+    """A 64-channel layer whose dA comes from a pool (with / without skip) or the heads: the BN state,
+    the dA source for selunet_conv3x3_wgrad_x2_bn_src, and a call of the standalone apply it replaces."""
+    n, h, w, c = 2, 20, 36, 64  # ragged 8x8 tiles in y
+    m = n * h * w
+    y = ((gen(m, c, seed=seed) * 2).round() / 2).to(DEV)  # coarse: ties inside the pool windows
+    sc, sh, mean, invstd, coef = coefs(c, seed + 1)
+    coef[0] = coef[0].abs() + 0.5
+    keep = []
+    if form.startswith("pool"):
+        dp = (gen(m // 4, c, seed=seed + 2) * 1e-2).to(DEV)
+        ds = (gen(m, c, seed=seed + 3) * 1e-2).to(DEV) if form == "pool" else None
+        keep += [dp, ds]
+        src = K.DaSource(K.DA_POOL, 0, K.ptr(dp), K.ptr(ds))
+
+        def apply(dy, am):
+            K.call("selunet_bn_bwd_apply_pool", K.ptr(y), n, h, w, c, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+                   K.ptr(coef), K.ptr(dp), K.ptr(ds), K.ptr(dy), K.ptr(am), K.F32, K.stream_ptr())
+    else:
+        nh = int(form[-1])
+        wt = (gen(3, 64, seed=seed + 4) * 0.2).to(DEV).contiguous()
+        g = [(gen(m, seed=seed + 5 + i) * 1e-3).to(DEV) for i in range(3)]
+        gp = [K.ptr(g[i]) if i < nh else None for i in range(3)]
+        keep += [wt, g]
+        src = K.DaSource(K.DA_HEADS, nh, None, None, K.ptr(wt), (ctypes.c_void_p * 3)(*gp))
+
+        def apply(dy, am):
+            K.call("selunet_bn_bwd_apply_heads", K.ptr(y), m, K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd),
+                   K.ptr(coef), K.ptr(wt), nh, *gp, K.ptr(dy), K.ptr(am), K.F32, K.stream_ptr())
+    return (n, h, w, c), (y, sc, sh, mean, invstd, coef), src, apply, keep
+
+
+@pytest.mark.parametrize("form", ["pool", "pool_noskip", "heads1", "heads3"])
+def test_wgrad_x2_bn_src_equals_apply_then_wgrad(form):
+    """selunet_conv3x3_wgrad_x2_bn_src with a pool / heads dA source (encoder_layer_1_2, decoder_layer_1_1)
+    against selunet_bn_bwd_apply_pool / _heads + selunet_conv3x3_wgrad_x2: dy and max |dy| identical, the
+    weight gradient within split-fp16 rounding of it and of the fp64 weight gradient."""
+    (n, h, w, c), (y, sc, sh, mean, invstd, coef), src, apply, _keep = _src_case(form)
+    m, ci = n * h * w, 64
+    x = gen(m, ci, seed=171).to(DEV)
+    xsc, xsh = (gen(ci, seed=172).abs() + 0.5).to(DEV), (gen(ci, seed=173) * 0.2).to(DEV)
+    xw = (torch.relu(x * xsc + xsh)).abs().max().reshape(1).contiguous()
+    gq = K.gather(n, h, w, 9, K.source(x, ci, xsc, xsh, relu=True, amax=xw))
+    dy0 = torch.empty(m, c, device=DEV)
+    am0 = torch.zeros(1, device=DEV)
+    apply(dy0, am0)
+    gp0 = K.gather(n, h, w, 1, K.source(dy0, c))
+    wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp0, gq)
+    ws = torch.empty(wsb // 4, device=DEV)
+    dw0 = torch.empty(c, ci, 3, 3, device=DEV)
+    K.call("selunet_conv3x3_wgrad_x2", gp0, gq, K.ptr(ws), wsb, K.ptr(dw0), K.ptr(am0), K.ptr(xw), None, K.stream_ptr())
+    torch.cuda.synchronize()
+    bound = (am0 * 37.0).contiguous()
+    dy1 = torch.full((m, c), float("nan"), device=DEV)
+    am1 = torch.zeros(1, device=DEV)
+    dw1 = torch.empty(c, ci, 3, 3, device=DEV)
+    gp1 = K.gather(n, h, w, 1, K.source(y, c))  # grid and channel count only
+    bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), None)
+    K.call("selunet_conv3x3_wgrad_x2_bn_src", gp1, gq, K.ptr(ws), wsb, K.ptr(dw1), K.ptr(bound), K.ptr(xw), None, bnb,
+           K.ptr(coef), src, K.ptr(dy1), K.ptr(am1), K.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dy1.cpu(), dy0.cpu())
+    assert am1.item() == am0.item()
+    xin = torch.relu(x.double() * xsc.double() + xsh.double()).reshape(n, h, w, ci).permute(0, 3, 1, 2)
+    g = dy0.double().reshape(n, h, w, c).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xin.cpu(), (c, ci, 3, 3), g.cpu(), padding=1)
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())  # noqa: E731
+    e0, e1 = rel(dw0.cpu(), ref), rel(dw1.cpu(), ref)
+    print(f"wgrad rel err unfused {e0:.2e} fused {e1:.2e}")
+    assert e1 < 2e-6 and e0 < 2e-6
+    assert rel(dw1.cpu(), dw0.cpu().double()) < 2e-6
+
+
+def test_wgrad_x2_bn_src_argument_checks():
+    (n, h, w, c), (y, sc, sh, mean, invstd, coef), src, _, _keep = _src_case("pool")
+    x = gen(n * h * w, 128, seed=181).to(DEV)
+    xw = x.abs().max().reshape(1).contiguous()
+    gq = K.gather(n, h, w, 9, K.source(x, 128, amax=xw))
+    y128 = torch.zeros(n * h * w, 128, device=DEV)
+    ws = torch.empty(1 << 24, device=DEV)
+    out = torch.empty(128, 128, 3, 3, device=DEV)
+    bnb = K.BnBwdStats(K.ptr(y128), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), None)
+    with pytest.raises(K.SelunetError):  # pool / heads sources are 64-channel forms
+        K.call("selunet_conv3x3_wgrad_x2_bn_src", K.gather(n, h, w, 1, K.source(y128, 128)), gq, K.ptr(ws),
+               ws.numel() * 4, K.ptr(out), K.ptr(xw), K.ptr(xw), None, bnb, K.ptr(coef), src, None, None,
+               K.stream_ptr())
+    bad = K.DaSource(7, 0, None, None)
+    bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), None)
+    with pytest.raises(K.SelunetError):
+        K.call("selunet_conv3x3_wgrad_x2_bn_src", K.gather(n, h, w, 1, K.source(y, 64)), gq, K.ptr(ws), ws.numel() * 4,
+               K.ptr(out), K.ptr(xw), K.ptr(xw), None, bnb, K.ptr(coef), bad, None, None, K.stream_ptr())
