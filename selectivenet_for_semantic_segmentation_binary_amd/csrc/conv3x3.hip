@@ -395,6 +395,17 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     }
   };
 
+  // a slice already transformed (X2: and split, high parts in .x/.y, low parts in .z/.w) in the last job
+  auto halo_store_prepped = [&](int hb, int hp, int cc, uint4 v) __attribute__((always_inline)) {
+    unsigned char* base = As + hb * HPIX * AROWB + hp * AROWB;
+    if constexpr (X2) {
+      const int par = (hp / HWT) & 1;
+      *reinterpret_cast<uint2*>(base + (((cc >> 1) ^ par) << 4) + (cc & 1) * 8) = make_uint2(v.x, v.y);
+      *reinterpret_cast<uint2*>(base + (((4 + (cc >> 1)) ^ par) << 4) + (cc & 1) * 8) = make_uint2(v.z, v.w);
+    } else {
+      *reinterpret_cast<uint4*>(base + (((cc ^ ((hp / HWT) & 1))) << 4)) = v;
+    }
+  };
   auto tile_xy = [&](int pt_i, int& img, int& y0, int& x0) __attribute__((always_inline)) {
     const unsigned pt = (unsigned)pt_i;
     const unsigned r = pt / (unsigned)tiles_x;
@@ -621,7 +632,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
       for (int t = 0; t < 9; ++t) {
         const int st2 = c * 9 + t + 2;  // weights are loaded two steps ahead
         const BRegs rb_far = b_load(st2 < csteps ? st2 : st2 - csteps);  // next tile's steps wrap
-        if (t == 0 && !defer && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
+        if (t == 0 && sn.scale && tid < 2 * CK) coef = tid < CK ? sn.scale[cs + tid] : sn.shift[cs + tid - CK];
 #pragma unroll
         for (int r = 0; r < A_ROUNDS; ++r) {
           if (halo_load_tap(r) == t) {
@@ -639,29 +650,47 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
         }
         if (defer && t == 8) rb_hold = rb_next;  // B(S + 1): stored after the epilogue
         else b_store(rb_next, (S + 1) & 1);
-        if (!defer) {
-          if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
+        if (t == 1 && sn.scale && tid < 2 * CK) (tid < CK ? ssc[tid] : ssh[tid - CK]) = coef;
 #pragma unroll
-          for (int r = 0; r < A_ROUNDS; ++r) {
-            if (halo_write_tap(r) != t) continue;
-            int hp, cc;
-            if (a_slot(r, hp, cc)) {
-              uint4 v = make_uint4(0, 0, 0, 0);
-              if (a_inside(ny0, nx0, hp)) {
-                v = ra[r];
-                if (sn.scale) {
-                  T e[E];
-                  __builtin_memcpy(e, &v, 16);
+        for (int r = 0; r < A_ROUNDS; ++r) {
+          if (halo_write_tap(r) != t) continue;
+          int hp, cc;
+          if (a_slot(r, hp, cc)) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (a_inside(ny0, nx0, hp)) {
+              v = ra[r];
+              if (sn.scale) {
+                T e[E];
+                __builtin_memcpy(e, &v, 16);
 #pragma unroll
-                  for (int j = 0; j < E; ++j) {
-                    float f = to_f(e[j]) * ssc[cc * E + j] + ssh[cc * E + j];
-                    if (sn.relu) f = fmaxf(f, 0.0f);
-                    e[j] = from_f<T>(f);
-                  }
-                  __builtin_memcpy(&v, e, 16);
+                for (int j = 0; j < E; ++j) {
+                  float f = to_f(e[j]) * ssc[cc * E + j] + ssh[cc * E + j];
+                  if (sn.relu) f = fmaxf(f, 0.0f);
+                  e[j] = from_f<T>(f);
                 }
+                __builtin_memcpy(&v, e, 16);
               }
+            }
+            if (!defer) {
               halo_store((J + 1) & 1, hp, cc, v);
+            } else {
+              // the next tile's first job: its slice is transformed (and split) here, under this job's
+              // MFMAs, and written to LDS after the epilogue (which uses the whole LDS) with no global reads
+              if constexpr (X2) {
+                float f[4];
+                __builtin_memcpy(f, &v, 16);
+                f16x4 h, l;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  _Float16 a, b;
+                  x2_split(f[e] * xs, a, b);
+                  h[e] = a;
+                  l[e] = b;
+                }
+                __builtin_memcpy(&v.x, &h, 8);
+                __builtin_memcpy(&v.z, &l, 8);
+              }
+              ra[r] = v;
             }
           }
         }
@@ -722,12 +751,15 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     }
     if (TQ ? pt_next < ptiles : i + 1 < ntl) {
       __syncthreads();  // the tile has been read: LDS back to halo / weights
-      int nimg, ny0, nx0;
-      tile_xy(TQ ? pt_next : prow + (i + 1) * gp, nimg, ny0, nx0);
-      int cs;
-      const SrcArg sn = chunk_src(0, cs);
+      // (slots recomputed from an opaque copy of tid: kept from the prologue they would be spilled, and a
+      // scratch reload here waits for every store of the epilogue above)
+      int tid2 = tid;
+      asm volatile("" : "+v"(tid2));
 #pragma unroll
-      for (int r = 0; r < A_ROUNDS; ++r) halo_put_global(ra[r], r, sn, cs, ny0, nx0, J & 1);
+      for (int r = 0; r < A_ROUNDS; ++r) {
+        const int hidx = r * HTHREADS + tid2;
+        if (hidx < HPIX * 8) halo_store_prepped(J & 1, hidx >> 3, hidx & 7, ra[r]);  // (transformed in the last job)
+      }
       b_store(rb_hold, S & 1);
       __syncthreads();
     }

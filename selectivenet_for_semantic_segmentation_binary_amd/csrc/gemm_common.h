@@ -290,6 +290,10 @@ __device__ __forceinline__ void lds_tile_store_acc(float* tile, int tid, Dst&& d
       is[e] = ts.bnb.invstd[col + e];
     }
   }
+  // Retire the coefficient loads above before the row loop: on gfx9 stores share vmcnt with loads, and a
+  // load still pending from before the loop makes the wait-count pass put s_waitcnt vmcnt(0) ahead of
+  // every row (its loop-header merge cannot count the stores in between) — one store round trip per row.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
   // per-tile fp32 partials; with fp32 accumulators they are the accumulators themselves
   constexpr bool WIDE = !std::is_same<Acc, float>::value;
   float tw1[WIDE ? 8 : 1] = {}, tw2[WIDE ? 8 : 1] = {}, tw3[WIDE ? 8 : 1] = {};
