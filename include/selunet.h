@@ -63,6 +63,9 @@ enum {
   SELUNET_OPT_TILE_QUEUE,         /* split-fp16 persistent 3x3 kernel: pixel tiles from a ticket counter, statistics
                                    * per tile (1), or the static walk (0, default); selunet_conv3x3_x2_stats_rows
                                    * follows it (robustness to a concurrent all-reduce) */
+  SELUNET_OPT_WGRAD_BN_BI,        /* column tile of the BN-fused split-fp16 weight gradient for outputs of 128+
+                                   * channels: 128 (0, default) or 64 (1: no half-tile staging, two k-steps of load
+                                   * cover); selunet_conv3x3_wgrad_x2_ws_bytes sizes for either */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an

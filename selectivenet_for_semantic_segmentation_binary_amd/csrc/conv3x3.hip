@@ -2251,9 +2251,14 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
   return check_launch("conv3x3_wgrad_wino");
 }
 
+// column tile of the split-fp16 weight gradient (bn: the BN-fused form, SELUNET_OPT_WGRAD_BN_BI)
+int conv3x3_wgrad_x2_bi(const GatherArg& p, bool bn) {
+  return p.K % 128 == 0 && !(bn && option(SELUNET_OPT_WGRAD_BN_BI, 0) == 1) ? 128 : 64;
+}
+
 // pixel-tile splits of the split-fp16 weight gradient: ~256 workgroups over (co tile, ci chunk, split)
-int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out) {
-  const int bi = p.K % 128 == 0 ? 128 : 64;
+int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out, bool bn) {
+  const int bi = conv3x3_wgrad_x2_bi(p, bn);
   const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
   const int64_t total = (int64_t)q.n * cdiv(q.w, XTW) * cdiv(q.h, XTH);
   const int64_t target = std::max<int64_t>(1, option(SELUNET_OPT_X2_WGRAD_WGS, 256));
@@ -2265,12 +2270,12 @@ int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t*
 
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
                             const float* amax_q0, const float* amax_q1, hipStream_t st, const WgradBnArg* bn) {
-  const int bi = p.K % 128 == 0 ? 128 : 64;
+  const int bi = conv3x3_wgrad_x2_bi(p, bn != nullptr);
   const int co_tiles = p.K / bi, ci_chunks = q.Ctot / 64;
   const int tiles_x = (int)cdiv(q.w, XTW), tiles_y = (int)cdiv(q.h, XTH);
   const int64_t total = (int64_t)q.n * tiles_x * tiles_y;
   int64_t per;
-  const int64_t splits = conv3x3_wgrad_x2_splits(p, q, &per);
+  const int64_t splits = conv3x3_wgrad_x2_splits(p, q, &per, bn != nullptr);
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
   const int kind = bn ? bn->kind : -1;
   SELUNET_REQUIRE(kind <= SELUNET_DA_TENSOR || bi == 64, "conv3x3_wgrad_x2: pool / heads dA sources need 64 columns");

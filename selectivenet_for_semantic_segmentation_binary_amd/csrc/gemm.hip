@@ -1530,19 +1530,19 @@ extern "C" int selunet_gemm_wgrad_ws_to(const selunet_gather* p, const selunet_g
 
 // fp32 3x3 weight gradient on split-fp16 operands (conv3x3_wgrad_x2_kernel + the fixed-order split
 // reduction into the Conv2d layout)
-static int plan_wgrad_x2(const selunet_gather* p, const selunet_gather* q, WgradPlan& w) {
+static int plan_wgrad_x2(const selunet_gather* p, const selunet_gather* q, WgradPlan& w, bool bn = false) {
   if (int rc = plan_wgrad(p, q, SELUNET_F32, w)) return rc;
   SELUNET_REQUIRE(halo_enabled() && conv3x3_wgrad_halo_eligible(w.gp, w.gq, SELUNET_F32) && w.gq.K % 9 == 0,
                   "conv3x3_wgrad_x2: operands not eligible (P: 1 tap, K %% 64 == 0; Q: 3x3, channels %% 64 == 0, "
                   "h >= 8, w >= 16)");
-  w.splits = conv3x3_wgrad_x2_splits(w.gp, w.gq, nullptr);
+  w.splits = conv3x3_wgrad_x2_splits(w.gp, w.gq, nullptr, bn);
   return 0;
 }
 
 extern "C" int64_t selunet_conv3x3_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q) {
-  WgradPlan w;
-  if (plan_wgrad_x2(p, q, w)) return -1;
-  return w.splits * (int64_t)w.ni * w.nj_pad * 4;
+  WgradPlan w, wb;  // (the plain and the BN-fused forms' splits may differ: SELUNET_OPT_WGRAD_BN_BI)
+  if (plan_wgrad_x2(p, q, w) || plan_wgrad_x2(p, q, wb, true)) return -1;
+  return std::max(w.splits, wb.splits) * (int64_t)w.ni * w.nj_pad * 4;
 }
 
 extern "C" int selunet_conv3x3_wgrad_x2(const selunet_gather* p, const selunet_gather* q, float* ws, int64_t ws_bytes,
@@ -1569,7 +1569,7 @@ extern "C" int selunet_conv3x3_wgrad_x2_bn_src(const selunet_gather* p, const se
                                                const float* amax_q1, const selunet_bn_bwd_stats* bnb, const float* coef,
                                                const selunet_da_source* src, float* dy, float* dy_amax, void* stream) {
   WgradPlan w;
-  if (int rc = plan_wgrad_x2(p, q, w)) return rc;
+  if (int rc = plan_wgrad_x2(p, q, w, true)) return rc;
   const int64_t need = w.splits * (int64_t)w.ni * w.nj_pad * 4;
   SELUNET_REQUIRE(out != nullptr && ws != nullptr && ws_bytes >= need, "conv3x3_wgrad_x2_bn: out / workspace of %lld bytes",
                   (long long)need);

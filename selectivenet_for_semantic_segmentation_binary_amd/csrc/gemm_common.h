@@ -489,7 +489,8 @@ int64_t conv3x3_x2d_rows(const GatherArg& g);
 int conv3x3_x2d_launch(const GatherArg& g, const float* w, const EpiArg& ep, const float* amax0, const float* amax1,
                        hipStream_t st);
 bool conv3x3_wgrad_halo_eligible(const GatherArg& p, const GatherArg& q, int dtype);
-int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out);
+int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out, bool bn = false);
+int conv3x3_wgrad_x2_bi(const GatherArg& p, bool bn);
 // SELUNET_OPT_TILE_QUEUE and the split-fp16 persistent kernel's statistics slab rows (conv3x3.hip)
 bool x2_tile_queue();
 int64_t conv3x3_x2_persist_rows(const GatherArg& g, int N);
