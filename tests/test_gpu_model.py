@@ -76,25 +76,36 @@ def check_step(d, s, r, strict, info=None):
     the number of flipped prediction-mask pixels."""
     selective = bool(d["meta_selective"])
     pre = f"s{s}/"
-    tol = 1e-4 if strict else 1e-2
+    # later steps (after one or more Adam steps): the loss to 1e-4 relative, logits to 5e-3 — measured
+    # 3e-6..1.5e-5 and 0.9e-3..1.8e-3 (profiles/r05k_later_steps.txt): Adam moves an element whose gradient
+    # sits at rounding level by +-lr either way, which the logits see at the 1e-3 level; the loss averages it
+    tol = 1e-4 if strict else 1e-4
+    tol_logits = 1e-4 if strict else 5e-3
     ref_loss = float(d[pre + "loss"])
     if info is not None:
         info["loss_rel_err"] = abs(r["loss"] - ref_loss) / max(1e-30, abs(ref_loss))
+    if not strict:  # (the later steps' measured deviation, for the record)
+        out_ref = d[pre + "output"] if pre + "output" in d.files else d[pre + "output_val"]
+        out_got = r["output"] if pre + "output" in d.files else r["output"].ravel()[d[pre + "output_idx"]]
+        print(f"{pre} loss rel err {abs(r['loss'] - ref_loss) / max(1e-30, abs(ref_loss)):.2e}, "
+              f"logits max rel {G.max_rel(out_got, out_ref):.2e}" +
+              "".join(f", {h} max rel {G.max_rel(r[h], d[pre + h]):.2e}" for h in ("selection", "aux")
+                      if h in r and pre + h in d.files))
     assert abs(r["loss"] - ref_loss) <= tol * max(1.0, abs(ref_loss)), (s, r["loss"], ref_loss)
     if selective:
         assert abs(r["coverage"] - float(d[pre + "coverage"])) <= tol
         for k in ("aux_loss", "select_loss"):
             assert abs(r[k] - float(d[pre + k])) <= tol * max(1.0, abs(float(d[pre + k]))), (k, r[k])
     if pre + "output" in d.files:
-        assert G.max_rel(r["output"], d[pre + "output"]) < tol
+        assert G.max_rel(r["output"], d[pre + "output"]) < tol_logits
     else:
         flat = r["output"].ravel()
-        assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol
+        assert G.max_rel(flat[d[pre + "output_idx"]], d[pre + "output_val"]) < tol_logits
     for h in ("selection", "aux"):
         if h in r and pre + h in d.files:
-            assert G.max_rel(r[h], d[pre + h]) < tol, h
+            assert G.max_rel(r[h], d[pre + h]) < tol_logits, h
         elif h in r and pre + h + "_idx" in d.files:
-            assert G.max_rel(r[h].ravel()[d[pre + h + "_idx"]], d[pre + h + "_val"]) < tol, h
+            assert G.max_rel(r[h].ravel()[d[pre + h + "_idx"]], d[pre + h + "_val"]) < tol_logits, h
     fails = []
     if strict:
         # prediction masks (train.py:150,153): report the flipped pixels; none may flip unless a
