@@ -186,7 +186,7 @@ class KernelTimer:
             else:  # reads y and the heads' gradient planes, writes dy
                 form, dab = "heads", self._src_bytes(gp) + 4.0 * m * src.nh
             nbytes = dab + self._src_bytes(gp) + self._src_bytes(gq) + 4 * self._k(gp) * self._k(gq)
-            return (f"conv3x3_wgrad_x2_{form}<64>+reduce", "mfma_f16", flops, nbytes,
+            return (f"conv3x3_wgrad_x2_{form}<{128 if self._k(gp) % 128 == 0 else 64}>+reduce", "mfma_f16", flops, nbytes,
                     f"wgrad x2 {form} {gp.h}x{gp.w} Kp={self._k(gp)} Kq={self._k(gq)}")
         if name == "selunet_gemm_wgrad_x2":  # (gp, gq, ws, wsb, layout, out, amax_p0, p1, q0, q1, stream)
             gp, gq = args[0], args[1]
