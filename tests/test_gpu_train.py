@@ -174,7 +174,7 @@ def test_miou_parity_vs_reference_training(dtype, tol, fname):
             zs[k] = (got - ens.mean()) / max(ens.std(ddof=1), 1e-9)
     line = (f"mIoU {fname} [{dtype}]: train {m_tr:.5f} (reference {m_tr_ref:.5f}), val {m_all:.5f} (reference "
             f"{float(d['val_miou']):.5f}), val selective {m_sel:.5f} (reference {float(d['val_miou_selective']):.5f}); "
-            f"reference spread {spread}; z vs the reference ensemble {({k: round(v, 2) for k, v in zs.items()})}; "
+            f"reference spread {spread}; z vs the reference ensemble {({k: round(float(v), 2) for k, v in zs.items()})}; "
             f"tol {tol}")
     print(line)
     G.SUMMARY.append(line)
