@@ -1647,7 +1647,7 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
       const bool more = pt + 1 < (int)pt_end;
       // the next tile goes to the free buffer in two halves (dY after k-step 1, the halo at the end),
       // so only one half's staging registers are live at a time (BNA at BI = 128: dA and y in two
-      // quarters, after k-steps 0 and 1)
+      // quarters, stored after k-steps 0 and 2)
       constexpr bool QSPLIT = BNA && BI == 128;
       constexpr int PH = QSPLIT ? P_ROUNDS / 2 : P_ROUNDS;
       load_p(more ? pt + 1 : pt, 0, PH);
@@ -1659,7 +1659,10 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
           load_p(more ? pt + 1 : pt, PH, P_ROUNDS);
           __builtin_amdgcn_sched_barrier(0);
         }
-        if (ks == 2) {
+        // (QSPLIT: the second dY half is stored at k-step 3, two k-steps after its loads, and the halo's loads get
+        // the last k-step — the halo rows are L2-hot more often: 1.5 % on the fused 128-column weight gradients,
+        // profiles/r05p_wgrad_bn_schedule_ab.txt)
+        if (ks == (QSPLIT ? 3 : 2)) {
           if (more) store_p(pt + 1, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
           load_x(more ? pt + 1 : pt);
           __builtin_amdgcn_sched_barrier(0);
