@@ -1661,10 +1661,16 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
         }
         // (QSPLIT: the second dY half is stored at k-step 3, two k-steps after its loads, and the halo's loads get
         // the last k-step — the halo rows are L2-hot more often: 1.5 % on the fused 128-column weight gradients,
-        // profiles/r05p_wgrad_bn_schedule_ab.txt)
-        if (ks == (QSPLIT ? 3 : 2)) {
-          if (more) store_p(pt + 1, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
+        // profiles/r05p_wgrad_bn_schedule_ab.txt. BI = 64, whose registers allow both operands in flight at once:
+        // the halo loaded at k-step 1 and the dY tile stored at k-step 3, three k-steps of cover each: 3-4 %,
+        // profiles/r05q_wgrad64_schedule_ab.txt)
+        if (BI == 64 && ks == 1) {
           load_x(more ? pt + 1 : pt);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (ks == (QSPLIT || BI == 64 ? 3 : 2)) {
+          if (more) store_p(pt + 1, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
+          if (BI != 64) load_x(more ? pt + 1 : pt);
           __builtin_amdgcn_sched_barrier(0);
         }
         const int prow = ks * 16 + 8 * half + q4;
