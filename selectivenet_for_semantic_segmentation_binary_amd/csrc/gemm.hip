@@ -1139,7 +1139,8 @@ static int x2_bn(int n_cols, const EpiArg& e) {
 // statistics slab rows (= persistent row workgroups) of the split-fp16 gather GEMM; independent of
 // the column tile width (128 / 256), like gather_rows. N not a multiple of 128: the 128-row kernel.
 static int64_t x2_rows(const GatherArg& g, int N) {
-  if (convt_dgrad_x2_ntb(g, N) > 0) return convt_dgrad_x2_rows(g, N);  // (whichever kernel the epilogue picks)
+  if (convt_ring_dgrad_operand_ok(g, N)) return convt_ring_rows(g, N);    // (whichever kernel the epilogue picks)
+  if (convt_dgrad_x2_ntb(g, N) > 0) return convt_dgrad_x2_rows(g, N);
   if (N % 128 != 0) return gather_rows(g, N);
   const int64_t m_tiles = cdiv(g.M, X2_BM);
   const int64_t wgs = gather_wgs();  // (the gather knob: half as many of these one-per-CU workgroups)
@@ -1164,6 +1165,8 @@ extern "C" int selunet_gemm_gather_x2(const selunet_gather* a, const float* w, i
   SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
                   "gemm_gather_x2: every source needs its range word (amax0, amax1)");
   hipStream_t st = as_stream(stream);
+  // unpool3 / unpool2 forward and data gradient (K >= 256, 256-column blocks): the LDS-DMA ring kernel
+  if (convt_ring_x2_takes(g, n_cols, e)) return convt_ring_x2_launch(g, w, n_cols, e, amax0, st);
   // the ConvTranspose2d forward (scatter epilogue): the resident-weight kernel (convt.hip)
   if (convt_x2_eligible(g, n_cols, e)) return convt_x2_launch(g, w, n_cols, e, amax0, st);
   // its data gradient (PLAIN, BN-backward sums): the resident-weight data-gradient kernel

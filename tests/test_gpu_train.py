@@ -185,7 +185,18 @@ def test_miou_parity_vs_reference_training(dtype, tol, fname):
         assert d["val_miou_ens"].size >= 8, d["val_miou_ens"].size
     assert abs(m_tr - m_tr_ref) <= tol
     for got, key in ((m_all, "val_miou"), (m_sel, "val_miou_selective")):
-        assert abs(got - float(d[key])) <= tol, (key, got, float(d[key]))
+        # against the reference's distribution where it was sampled: one 16-epoch run is one draw of a chaotic
+        # process (the reference's own members sit up to 0.0021 from its unperturbed run on miou_sel_256s, so
+        # a single-run bar would fail the reference itself); the bar is on the ensemble mean, and ours must
+        # also lie inside the ensemble's 3-sigma band (fp32: the same arithmetic class as the reference's runs;
+        # bf16 is held to its wider bar alone)
+        if key + "_ens" in d.files:
+            ens = np.concatenate([[float(d[key])], d[key + "_ens"]])
+            assert abs(got - ens.mean()) <= tol, (key, got, float(ens.mean()))
+            if dtype == torch.float32:
+                assert abs(zs[key]) <= 3.0, (key, got, zs[key])
+        else:
+            assert abs(got - float(d[key])) <= tol, (key, got, float(d[key]))
     if fname == "miou_sel_256s.npz":
         # the selective metric is not degenerate here, and the selection keeps as many pixels as the reference's
         assert 0.85 <= float(d["val_miou_selective"]) <= 0.99, float(d["val_miou_selective"])

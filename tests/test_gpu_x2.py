@@ -446,6 +446,106 @@ def test_x2_convT_dgrad_resident(cin, cout, n, h, w):
         assert float(err.max()) < 1e-6, (k, float(err.max()))
 
 
+@pytest.fixture
+def convt_ring():
+    """Set SELUNET_OPT_CONVT_RING for one test (0: the resident-weight / staged kernels)."""
+    prev = []
+
+    def setter(mode):
+        prev.append(K.set_option("CONVT_RING", mode))
+    yield setter
+    for v in prev[:1]:
+        K.set_option("CONVT_RING", v)
+
+
+def _convT_x2_pair(cin, cout, n, h, w, seed):
+    """Forward (+ bias, range word) and data gradient (+ BN-backward sums, range word) of one
+    ConvTranspose2d through selunet_gemm_gather_x2 with whatever kernels the options select."""
+    x = gen(n, cin, h, w, seed=seed)
+    s, t = bn_fold(cin, seed + 1)
+    wt = gen(cin, cout, 2, 2, seed=seed + 2, scale=0.05)
+    b = gen(cout, seed=seed + 3)
+    dy = gen(n, cout, 2 * h, 2 * w, seed=seed + 4) * 1e-3
+    fwd, dg = pack_convT_x2(wt)
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    xd, sd, td, bd = d(nhwc(x)), d(s), d(t), d(b)
+    M = n * h * w
+    up = torch.empty(M * 4, cout, device=DEV)
+    amu = torch.zeros(1, device=DEV)
+    ep = K.Epilogue(K.ptr(up), None, K.ptr(bd), None, K.EP_SCATTER2X, 0)
+    ep.amax = K.ptr(amu)
+    am = word(torch.relu(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1)).abs().max())
+    K.call("selunet_gemm_gather_x2", K.gather(n, h, w, 1, K.source(xd, cin, sd, td)), K.ptr(fwd), 4 * cout, cin, ep,
+           K.ptr(am), None, K.stream_ptr())
+    dud = d(nhwc(dy))
+    amd = word(dy.abs().max())
+    da = torch.empty(M, cin, device=DEV)
+    yprev = gen(M, cin, seed=seed + 5).to(DEV)
+    sc, sh = (gen(cin, seed=seed + 6).abs() + 0.5).to(DEV), (gen(cin, seed=seed + 7) * 0.3).to(DEV)
+    mean, invstd = (gen(cin, seed=seed + 8) * 0.1).to(DEV), (gen(cin, seed=seed + 9).abs() + 0.5).to(DEV)
+    g4 = K.gather(n, h, w, 4, K.source(dud, cout))
+    rows = K.query("selunet_gemm_gather_x2_stats_rows", g4, cin)
+    slab = torch.full((rows, 3, cin), float("nan"), device=DEV)
+    amo = torch.zeros(1, device=DEV)
+    ep = K.Epilogue(K.ptr(da), None, None, None, K.EP_PLAIN, 0)
+    ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+    ep.amax = K.ptr(amo)
+    K.call("selunet_gemm_gather_x2", g4, K.ptr(dg), cin, 4 * cout, ep, K.ptr(amd), None, K.stream_ptr())
+    torch.cuda.synchronize()
+    return dict(x=x, s=s, t=t, wt=wt, b=b, dy=dy, up=up, amu=amu, da=da, amo=amo, slab=slab, rows=rows,
+                yprev=yprev, sc=sc, sh=sh, mean=mean, invstd=invstd)
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [
+    (512, 256, 2, 32, 32),    # unpool3 at a 2-image shard: forward K 512 / N 1024, data gradient K 1024 / N 512
+    (256, 128, 1, 64, 64),    # unpool2: forward K 256 / N 512, data gradient K 512 / N 256
+    (512, 256, 1, 16, 32),    # one row tile: more column blocks than row tiles
+])
+def test_x2_convT_ring(cin, cout, n, h, w, convt_ring):
+    """The LDS-DMA ring kernel (convt_ring_x2_kernel, ConvTranspose2d forward and data gradient with
+    K >= 256 on 256-column blocks) against torch in fp64: output, output range word, and the
+    BN-backward sums against the sums of its own output (one slab row per ring workgroup)."""
+    convt_ring(1)
+    r = _convT_x2_pair(cin, cout, n, h, w, seed=60)
+    a = torch.relu(r["x"] * r["s"].view(1, -1, 1, 1) + r["t"].view(1, -1, 1, 1)).double().requires_grad_()
+    y = F.conv_transpose2d(a, r["wt"].double(), r["b"].double(), stride=2)
+    (ga,) = torch.autograd.grad(y, (a,), r["dy"].double())
+    assert rel(nchw(r["up"].cpu(), n, 2 * h, 2 * w), y.detach()) < TOL
+    assert r["amu"].item() == r["up"].abs().max().item()
+    assert rel(nchw(r["da"].cpu(), n, h, w), ga) < TOL
+    assert r["amo"].item() == r["da"].abs().max().item()
+    M = n * h * w
+    blocks = cin // 256
+    assert r["rows"] == min(M // 256, max(1, 256 // blocks))  # the ring kernel's workgroup rows
+    y64, sc, sh = r["yprev"].double(), r["sc"].double(), r["sh"].double()
+    g64 = r["da"].double() * (y64 * sc + sh > 0).double()
+    xh = (y64 - r["mean"].double()) * r["invstd"].double()
+    got = r["slab"].double().sum(0)
+    for k, term in enumerate([g64, g64 * xh, xh]):
+        err = (got[k] - term.sum(0)).abs() / (term.abs().sum(0) + 1e-30)
+        assert float(err.max()) < 1e-6, (k, float(err.max()))
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [
+    (512, 256, 4, 32, 32),
+    (256, 128, 4, 128, 160),  # data gradient: 320 row tiles on 256 workgroups (two tiles for some)
+    (512, 256, 16, 32, 96),   # forward: 4 column blocks x 64 workgroup rows over 192 row tiles
+])
+def test_x2_convT_ring_matches_resident(cin, cout, n, h, w, convt_ring):
+    """The ring kernel computes the products and sums of the resident-weight / staged kernels in the same
+    order (hl, lh, hh per 16-k step, k ascending): forward and data gradient outputs bit-identical with
+    SELUNET_OPT_CONVT_RING on and off, also where workgroups walk several row tiles."""
+    convt_ring(0)
+    off = _convT_x2_pair(cin, cout, n, h, w, seed=70)
+    convt_ring(1)
+    on = _convT_x2_pair(cin, cout, n, h, w, seed=70)
+    assert torch.equal(on["up"], off["up"])
+    assert torch.equal(on["da"], off["da"])
+    assert on["amu"].item() == off["amu"].item() and on["amo"].item() == off["amo"].item()
+    sums = lambda r: r["slab"].double().sum(0)  # noqa: E731
+    assert rel(sums(on), sums(off)) < 1e-6
+
+
 @pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64), (256, 128)])
 def test_x2_convT_wgrad(cin, cout):
     """ConvTranspose2d weight gradient through selunet_gemm_wgrad_x2 (split partials reduced into the
