@@ -67,7 +67,8 @@ enum {
                                    * channels: 128 (0, default) or 64 (1: no half-tile staging, two k-steps of load
                                    * cover); selunet_conv3x3_wgrad_x2_ws_bytes sizes for either */
   SELUNET_OPT_CONVT_RING,         /* fp32 ConvTranspose2d forward / data gradient with K >= 256 on 256-column blocks:
-                                   * the LDS-DMA ring kernel (1, default) or the resident-weight / staged kernels (0);
+                                   * the LDS-DMA ring kernel with the forward on 8 x 1 waves (2, default) or 4 x 2
+                                   * waves (1), or the resident-weight / staged kernels (0);
                                    * selunet_gemm_gather_x2_stats_rows follows it */
   SELUNET_OPT_COUNT
 };

@@ -40,12 +40,16 @@ constexpr int CR_KMAX = 1024;                         // forward coefficient are
 // loads logical slot cr_slot(r, p))
 __device__ __forceinline__ int cr_slot(int r, int s) { return s ^ ((r >> 2) & 3); }
 
-template <bool DGRAD>
+// WN: waves along the columns (2: 4 x 2 waves of 64 x 128; 1: 8 x 1 waves of 32 x 256, each A value split
+// by one wave, twice the B fragment reads — the forward's default, 3-5 % faster than 4 x 2 on the same box,
+// profiles/r05w_convt_ring_ab.txt; the data gradient keeps 4 x 2: its BN sums are carried per wave row in LDS)
+template <bool DGRAD, int WN = 2>
 __global__ void __launch_bounds__(CR_THREADS, 1)
 convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_blocks, int P,
                      const float* __restrict__ wcs, const float* __restrict__ amax_src, float* __restrict__ out,
                      const float* __restrict__ bias, float* amax_out, const float* __restrict__ ybn, BnBwdArg bnb) {
-  constexpr int MT = 2, NT = 4;
+  static_assert(WN == 2 || (WN == 1 && !DGRAD), "8 x 1 waves: forward only");
+  constexpr int MT = WN, NT = 8 / WN, WR = 32 * WN, WC = 256 / WN;  // subtiles, rows / columns per wave
   // past the ring: forward: the source's BN scale / shift x 2^e per k, the columns' unscale and bias;
   // data gradient: the columns' unscale and BN coefficients, and the fp64 BN-backward sums per (wave row,
   // column) carried across tiles (registers are full: 128 accumulators + the split A and B fragments)
@@ -59,7 +63,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = lane >> 5, l32 = lane & 31;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
   const int nb = (int)(lb % (unsigned)n_blocks);
   const int prow = (int)(lb / (unsigned)n_blocks);
@@ -74,7 +78,8 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
 
   float inv;
   const float xs = x2_scale(amax_src[0], &inv);
-  const bool relu = !DGRAD && g.src[0].scale != nullptr && g.src[0].relu;
+  // ReLU as a max against 0 (or -inf: no ReLU) — one v_max per element instead of a select on a runtime flag
+  const float relu_lo = !DGRAD && g.src[0].scale != nullptr && g.src[0].relu ? 0.0f : -INFINITY;
   if constexpr (!DGRAD) {
     const SrcArg& s0 = g.src[0];
     for (int c = tid; c < K; c += CR_THREADS) {
@@ -164,7 +169,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
     f16x8 bh[NT], bl[NT];
 #pragma unroll
     for (int b = 0; b < NT; ++b) {
-      const int n = wn * 128 + b * 32 + l32;
+      const int n = wn * WC + b * 32 + l32;
       bh[b] = *reinterpret_cast<const f16x8*>(sb + n * CR_ROWB + cr_slot(n, half) * 16);
       bl[b] = *reinterpret_cast<const f16x8*>(sb + n * CR_ROWB + cr_slot(n, 2 + half) * 16);
     }
@@ -183,7 +188,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
     }
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
-      const int r = wm * 64 + a * 32 + l32;
+      const int r = wm * WR + a * 32 + l32;
       const f32x4 v0 = *reinterpret_cast<const f32x4*>(sa + r * CR_ROWB + cr_slot(r, 2 * half) * 16);
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(sa + r * CR_ROWB + cr_slot(r, 2 * half + 1) * 16);
       f16x8 ah, al;
@@ -194,8 +199,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
         if constexpr (DGRAD) {
           f = v * xs;
         } else {
-          f = v * sc[e] + sh[e];  // (xs = 2^e > 0: relu(x) * xs == relu(x * xs), exactly)
-          if (relu) f = fmaxf(f, 0.0f);
+          f = fmaxf(v * sc[e] + sh[e], relu_lo);  // (xs = 2^e > 0: relu(x) * xs == relu(x * xs), exactly)
         }
         _Float16 hh, ll;
         x2_split(f, hh, ll);
@@ -219,13 +223,13 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
 #pragma unroll
       for (int a = 0; a < MT; ++a) {
         // subtile a: pixels r0 .. r0 + 31 of one image row (w % 32 == 0), x0 = r0 % w
-        const int64_t r0 = m_base + wm * 64 + a * 32;
+        const int64_t r0 = m_base + wm * WR + a * 32;
         const unsigned mu = (unsigned)r0, x0 = mu % (unsigned)g.w, tt = mu / (unsigned)g.w;
         const unsigned y = tt % (unsigned)g.h, img = tt / (unsigned)g.h;
         const int64_t row_even = ((int64_t)img * (2 * g.h) + 2 * y) * (2 * g.w);  // output row 2y
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
-          const int cl = wn * 128 + b * 32 + l32, n = n0 + cl;
+          const int cl = wn * WC + b * 32 + l32, n = n0 + cl;
           const int ab = n / Cq, o = n - ab * Cq;
           const int64_t base = row_even + (int64_t)(ab >> 1) * (2 * g.w) + (ab & 1);
           const float cf = ccol[cl], cb = ccol[CR_BN + cl];
@@ -244,10 +248,10 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
       for (int b = 0; b < NT; ++b) s1[b] = s2[b] = s3[b] = 0.0f;
 #pragma unroll
       for (int a = 0; a < MT; ++a) {
-        const int64_t r0 = m_base + wm * 64 + a * 32;
+        const int64_t r0 = m_base + wm * WR + a * 32;
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
-          const int cl = wn * 128 + b * 32 + l32;
+          const int cl = wn * WC + b * 32 + l32;
           const int64_t n = n0 + cl;
           const float cf = ccol[cl];
           const float* yp = ybn + (r0 + 4 * half) * N + n;
@@ -285,7 +289,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
           const float t1 = s1[b] + __shfl_xor(s1[b], 32, 64), t2 = s2[b] + __shfl_xor(s2[b], 32, 64);
           const float t3 = s3[b] + __shfl_xor(s3[b], 32, 64);
           if (half == 0) {
-            double* q = qacc + (wm * CR_BN + wn * 128 + b * 32 + l32) * 3;
+            double* q = qacc + (wm * CR_BN + wn * WC + b * 32 + l32) * 3;
             q[0] += (double)t1;
             q[1] += (double)t2;
             q[2] += (double)t3;
@@ -331,7 +335,7 @@ convt_ring_x2_kernel(GatherArg g, const float* __restrict__ W, int N, int n_bloc
 }
 
 // --------------------------------------------------------------------------- host side
-static bool ring_on() { return option(SELUNET_OPT_CONVT_RING, 1) != 0; }
+static bool ring_on() { return option(SELUNET_OPT_CONVT_RING, 2) != 0; }
 
 // the forward operand / epilogue this kernel takes (ConvTranspose2d forward, K = C_in of 256..1024)
 static bool convt_ring_fwd_ok(const GatherArg& g, int N, const EpiArg& e) {
@@ -381,7 +385,10 @@ int convt_ring_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg
   const float* wcs = w + (int64_t)N * g.K;
   const dim3 grid((unsigned)(P * blocks)), block(CR_THREADS);
   float* out = reinterpret_cast<float*>(e.out0);
-  if (fwd)
+  if (fwd && option(SELUNET_OPT_CONVT_RING, 2) == 2)
+    hipLaunchKernelGGL((convt_ring_x2_kernel<false, 1>), grid, block, 0, st, g, w, N, blocks, (int)P, wcs, amax_src,
+                       out, e.bias, e.amax, nullptr, BnBwdArg{});
+  else if (fwd)
     hipLaunchKernelGGL((convt_ring_x2_kernel<false>), grid, block, 0, st, g, w, N, blocks, (int)P, wcs, amax_src, out,
                        e.bias, e.amax, nullptr, BnBwdArg{});
   else

@@ -505,7 +505,7 @@ def test_x2_convT_ring(cin, cout, n, h, w, convt_ring):
     """The LDS-DMA ring kernel (convt_ring_x2_kernel, ConvTranspose2d forward and data gradient with
     K >= 256 on 256-column blocks) against torch in fp64: output, output range word, and the
     BN-backward sums against the sums of its own output (one slab row per ring workgroup)."""
-    convt_ring(1)
+    convt_ring(2)
     r = _convT_x2_pair(cin, cout, n, h, w, seed=60)
     a = torch.relu(r["x"] * r["s"].view(1, -1, 1, 1) + r["t"].view(1, -1, 1, 1)).double().requires_grad_()
     y = F.conv_transpose2d(a, r["wt"].double(), r["b"].double(), stride=2)
@@ -531,13 +531,14 @@ def test_x2_convT_ring(cin, cout, n, h, w, convt_ring):
     (256, 128, 4, 128, 160),  # data gradient: 320 row tiles on 256 workgroups (two tiles for some)
     (512, 256, 16, 32, 96),   # forward: 4 column blocks x 64 workgroup rows over 192 row tiles
 ])
-def test_x2_convT_ring_matches_resident(cin, cout, n, h, w, convt_ring):
+@pytest.mark.parametrize("mode", [1, 2])  # 2 (default): the forward on 8 x 1 waves
+def test_x2_convT_ring_matches_resident(cin, cout, n, h, w, mode, convt_ring):
     """The ring kernel computes the products and sums of the resident-weight / staged kernels in the same
     order (hl, lh, hh per 16-k step, k ascending): forward and data gradient outputs bit-identical with
     SELUNET_OPT_CONVT_RING on and off, also where workgroups walk several row tiles."""
     convt_ring(0)
     off = _convT_x2_pair(cin, cout, n, h, w, seed=70)
-    convt_ring(1)
+    convt_ring(mode)
     on = _convT_x2_pair(cin, cout, n, h, w, seed=70)
     assert torch.equal(on["up"], off["up"])
     assert torch.equal(on["da"], off["da"])
