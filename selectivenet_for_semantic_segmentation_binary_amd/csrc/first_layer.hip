@@ -326,10 +326,12 @@ first_conv_wgrad_kernel(const float* __restrict__ x, int cin, int h, int w, cons
   if (jobs > 0) {
     Loaded cur = load(0);
     for (int j = 0; j < jobs; ++j) {
+      // the next job's loads go out before this job's staging: a whole job of cover (two register sets)
+      const Loaded nxt = load(j + 1 < jobs ? j + 1 : j);
       stage(cur, j);
       __syncthreads();  // Xs, Ds written
       build_cols(j % NS);
-      if (j + 1 < jobs) cur = load(j + 1);
+      cur = nxt;
       __syncthreads();  // Cs written
       // out[co][k] += sum over this wave's 32 pixels of the stage
 #pragma unroll
