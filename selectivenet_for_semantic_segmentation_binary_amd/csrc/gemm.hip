@@ -529,14 +529,18 @@ gemm_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int64_t mchunk, int tile
   const SrcArg psa = pick_src(P, ps), qsa = pick_src(Q, qs);
   const float sp = x2_scale((ps ? amax_p1 : amax_p0)[0], nullptr);
   const float sq = x2_scale((qs ? amax_q1 : amax_q0)[0], nullptr);
+  // BN scale / shift with the operand's 2^e folded in (relu(x) 2^e == relu(x 2^e), and fma(x, sc 2^e, sh 2^e)
+  // == 2^e fma(x, sc, sh) exactly: the same values as scaling after the transform, one multiply fewer)
   float psc[4], psh[4], qsc[4], qsh[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    psc[e] = psa.scale && pin ? psa.scale[pch + e] : 1.0f;
-    psh[e] = psa.scale && pin ? psa.shift[pch + e] : 0.0f;
-    qsc[e] = qsa.scale && qin ? qsa.scale[qch + e] : 1.0f;
-    qsh[e] = qsa.scale && qin ? qsa.shift[qch + e] : 0.0f;
+    psc[e] = (psa.scale && pin ? psa.scale[pch + e] : 1.0f) * sp;
+    psh[e] = (psa.scale && pin ? psa.shift[pch + e] : 0.0f) * sp;
+    qsc[e] = (qsa.scale && qin ? qsa.scale[qch + e] : 1.0f) * sq;
+    qsh[e] = (qsa.scale && qin ? qsa.shift[qch + e] : 0.0f) * sq;
   }
+  const float plo = psa.scale && psa.relu ? 0.0f : -INFINITY;  // ReLU as one max (no per-element select)
+  const float qlo = qsa.scale && qsa.relu ? 0.0f : -INFINITY;
   float4 rp[PI], rq[PJ];
   unsigned pok = 0, qok = 0;  // bit i: staged row i is a real (non-padding) pixel
   auto raw_row = [&](const GatherArg& g, const SrcArg& sa, int64_t m, int tap, int c, bool in, unsigned& ok,
@@ -546,39 +550,54 @@ gemm_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int64_t mchunk, int tile
     pix = pix >= 0 ? pix : 0;
     return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(sa.data) + pix * sa.C + c);
   };
-  auto put = [&](float4 raw, bool ok, const SrcArg& sa, const float* sc, const float* sh, float s, _Float16* hp,
+  auto put = [&](float4 raw, bool ok, const SrcArg& sa, const float* sc, const float* sh, float lo, _Float16* hp,
                  _Float16* lp) __attribute__((always_inline)) {
     float f[4] = {raw.x, raw.y, raw.z, raw.w};
     f16x4 h, l;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float t = f[e];
-      if (sa.scale) {
-        t = t * sc[e] + sh[e];
-        if (sa.relu) t = fmaxf(t, 0.0f);
-      }
       _Float16 a, b;
-      x2_split(ok ? t * s : 0.0f, a, b);
+      x2_split(ok ? fmaxf(f[e] * sc[e] + sh[e], lo) : 0.0f, a, b);
       h[e] = a;
       l[e] = b;
     }
     *reinterpret_cast<f16x4*>(hp) = h;
     *reinterpret_cast<f16x4*>(lp) = l;
   };
+  // A stage's KM rows are KM consecutive pixels; when every stage starts a KM-pixel run inside one image row
+  // (w % KM == 0, split starts on stage boundaries) the 2x2-tap gather of Q needs one pixel decode per stage
+  // instead of one per staged row (the per-row divisions outweighed the MFMAs in the stage's vector issue)
+  const bool q_run = Q.taps == 4 && Q.w % KM == 0 && mchunk % KM == 0 && P.taps == 1;
   auto load_stage = [&](int64_t m_base) __attribute__((always_inline)) {
     pok = qok = 0;
 #pragma unroll
     for (int i = 0; i < PI; ++i) rp[i] = raw_row(P, psa, m_base + pr + RPI * i, ptap, pch, pin, pok, i);
+    if (q_run) {
+      const unsigned mu = (unsigned)m_base, x0 = mu % (unsigned)Q.w, t = mu / (unsigned)Q.w;
+      const unsigned y = t % (unsigned)Q.h, img = t / (unsigned)Q.h;
+      int dy, dx;
+      tap_offset(4, qtap, dy, dx);
+      const int64_t row0 = (((int64_t)img * Q.hs + 2 * y + dy) * Q.ws + 2 * x0 + dx) * qsa.C + qch;
 #pragma unroll
-    for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+      for (int i = 0; i < PJ; ++i) {
+        const int r = qr + RPJ * i;
+        const bool ok = qin && m_base + r < me;
+        qok |= (ok ? 1u : 0u) << i;
+        rq[i] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(qsa.data) +
+                                                 (ok ? row0 + (int64_t)(2 * r) * qsa.C : 0));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+    }
   };
   auto store_stage = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PI; ++i)
-      put(rp[i], (pok >> i) & 1u, psa, psc, psh, sp, &Ps[buf][0][pr + RPI * i][pc * 4], &Ps[buf][1][pr + RPI * i][pc * 4]);
+      put(rp[i], (pok >> i) & 1u, psa, psc, psh, plo, &Ps[buf][0][pr + RPI * i][pc * 4], &Ps[buf][1][pr + RPI * i][pc * 4]);
 #pragma unroll
     for (int i = 0; i < PJ; ++i)
-      put(rq[i], (qok >> i) & 1u, qsa, qsc, qsh, sq, &Qs[buf][0][qr + RPJ * i][qc * 4], &Qs[buf][1][qr + RPJ * i][qc * 4]);
+      put(rq[i], (qok >> i) & 1u, qsa, qsc, qsh, qlo, &Qs[buf][0][qr + RPJ * i][qc * 4], &Qs[buf][1][qr + RPJ * i][qc * 4]);
   };
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   auto tr8 = [&](const _Float16* p0, const _Float16* p1) __attribute__((always_inline)) {

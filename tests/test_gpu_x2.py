@@ -548,10 +548,10 @@ def test_x2_convT_ring_matches_resident(cin, cout, n, h, w, mode, convt_ring):
 
 
 @pytest.mark.parametrize("cin,cout", [(512, 256), (128, 64), (256, 128)])
-def test_x2_convT_wgrad(cin, cout):
+@pytest.mark.parametrize("n,h,w", [(2, 13, 18), (2, 9, 32), (1, 6, 64)])  # w % 32 == 0: one dU decode per stage
+def test_x2_convT_wgrad(cin, cout, n, h, w):
     """ConvTranspose2d weight gradient through selunet_gemm_wgrad_x2 (split partials reduced into the
     [ci][co][2][2] layout) against torch in fp64; bit-reproducible."""
-    n, h, w = 2, 13, 18
     x = gen(n, cin, h, w, seed=13)
     s, t = bn_fold(cin, 30)
     a = torch.relu(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1)).double()
