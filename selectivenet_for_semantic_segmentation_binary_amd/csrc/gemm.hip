@@ -792,13 +792,31 @@ gemm_wgrad_bf16_kernel(GatherArg P, GatherArg Q, float* __restrict__ out, int ld
     __builtin_memcpy(&raw, v, 16);
     return raw;
   };
+  // one dU pixel decode per stage where a stage's KM pixels are one run of an image row (gemm_wgrad_x2_kernel)
+  const bool q_run = !SMALL && Q.taps == 4 && Q.w % KM == 0 && mchunk % KM == 0 && P.taps == 1;
   auto load_stage = [&](int64_t m_base) {
     if constexpr (!SMALL) {
       pok = qok = 0;
 #pragma unroll
       for (int i = 0; i < PI; ++i) rp[i] = raw_row(P, psa, m_base + pr + RPI * i, ptap, pch, pin, pok, i);
+      if (q_run) {
+        const unsigned mu = (unsigned)m_base, x0 = mu % (unsigned)Q.w, t = mu / (unsigned)Q.w;
+        const unsigned y = t % (unsigned)Q.h, img = t / (unsigned)Q.h;
+        int dy, dx;
+        tap_offset(4, qtap, dy, dx);
+        const int64_t row0 = (((int64_t)img * Q.hs + 2 * y + dy) * Q.ws + 2 * x0 + dx) * qsa.C + qch;
 #pragma unroll
-      for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+        for (int i = 0; i < PJ; ++i) {
+          const int r = qr + RPJ * i;
+          const bool ok = qin && m_base + r < me;
+          qok |= (ok ? 1u : 0u) << i;
+          rq[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(qsa.data) +
+                                                  (ok ? row0 + (int64_t)(2 * r) * qsa.C : 0));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < PJ; ++i) rq[i] = raw_row(Q, qsa, m_base + qr + RPJ * i, qtap, qch, qin, qok, i);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < PI; ++i) {

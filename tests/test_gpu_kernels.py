@@ -617,10 +617,10 @@ def test_conv3x3_bf16_fwd_wgrad(cin0, cin1, cout, small, h, w, wgs, halo_wgs):
 
 
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 4, 6, 256, 128), (4, 16, 24, 128, 64), (3, 10, 14, 512, 256),
-                                             (2, 6, 10, 64, 64)])
+                                             (2, 6, 10, 64, 64), (2, 5, 64, 256, 128), (1, 3, 128, 128, 64)])
 def test_convT_bf16_wgrad(n, h, w, cin, cout):
     """The 256-column tiles (512 threads; 256 x 256 and 128 x 256) with several pixel splits and a ragged
-    last one, and the 128-column kernel (64 x 64)."""
+    last one, and the 128-column kernel (64 x 64); w % 64 == 0: one dU pixel decode per 64-pixel stage."""
     x = _bf(gen(n, cin, h, w, seed=45))
     wt = gen(cin, cout, 2, 2, seed=46, scale=0.05).requires_grad_()
     y = F.conv_transpose2d(x, wt, stride=2)
