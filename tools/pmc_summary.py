@@ -29,6 +29,7 @@ def _pat(base, *targs):
 NAME_MAP = [
     (r"gemm_gather_kernelIfLi(128|64)ELb0ELb1E|gemm_gather_kernel<float, (128|64), false, true", "gemm_gather_x2<f32>"),
     (r"convt_x2_kernel", "gemm_gather_x2<f32>"),  # (the resident-weight ConvTranspose2d forward, same entry point)
+    (r"convt_ring_x2_kernel", "gemm_gather_x2<f32>"),  # (the LDS-DMA ring ConvTranspose2d kernel, same entry point)
     (r"gemm_wgrad_x2_kernel", "gemm_wgrad_x2<f32>"),
     (_pat("conv3x3_halo_persist_kernel", "f32", 128, "true"), "conv3x3_x2<f32,128>"),
     (_pat("conv3x3_halo_persist_kernel", "f32", 64, "true"), "conv3x3_x2<f32,64>"),
