@@ -526,6 +526,39 @@ def test_x2_convT_ring(cin, cout, n, h, w, convt_ring):
         assert float(err.max()) < 1e-6, (k, float(err.max()))
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_x2_convT_ring_plain_operands(mode, convt_ring):
+    """The ring kernel without the optional parts: a forward source with no BN+ReLU transform and no bias,
+    a data gradient with no BN-backward sums (no slab) — against torch in fp64, with both range words."""
+    convt_ring(mode)
+    cin, cout, n, h, w = 256, 128, 2, 32, 32
+    x = gen(n, cin, h, w, seed=81)
+    wt = gen(cin, cout, 2, 2, seed=82, scale=0.05)
+    dy = gen(n, cout, 2 * h, 2 * w, seed=83)
+    fwd, dg = pack_convT_x2(wt)
+    d = lambda t_: t_.to(DEV).contiguous()  # noqa: E731
+    xd, dud = d(nhwc(x)), d(nhwc(dy))
+    M = n * h * w
+    up = torch.empty(4 * M, cout, device=DEV)
+    amu, amo = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    ep = K.Epilogue(K.ptr(up), None, None, None, K.EP_SCATTER2X, 0)
+    ep.amax = K.ptr(amu)
+    K.call("selunet_gemm_gather_x2", K.gather(n, h, w, 1, K.source(xd, cin)), K.ptr(fwd), 4 * cout, cin, ep,
+           K.ptr(word(x.abs().max())), None, K.stream_ptr())
+    da = torch.empty(M, cin, device=DEV)
+    ep = K.Epilogue(K.ptr(da), None, None, None, K.EP_PLAIN, 0)
+    ep.amax = K.ptr(amo)
+    K.call("selunet_gemm_gather_x2", K.gather(n, h, w, 4, K.source(dud, cout)), K.ptr(dg), cin, 4 * cout, ep,
+           K.ptr(word(dy.abs().max())), None, K.stream_ptr())
+    torch.cuda.synchronize()
+    a = x.double().requires_grad_()
+    y = F.conv_transpose2d(a, wt.double(), None, stride=2)
+    (ga,) = torch.autograd.grad(y, (a,), dy.double())
+    assert rel(nchw(up.cpu(), n, 2 * h, 2 * w), y.detach()) < TOL
+    assert rel(nchw(da.cpu(), n, h, w), ga) < TOL
+    assert amu.item() == up.abs().max().item() and amo.item() == da.abs().max().item()
+
+
 @pytest.mark.parametrize("cin,cout,n,h,w", [
     (512, 256, 4, 32, 32),
     (256, 128, 4, 128, 160),  # data gradient: 320 row tiles on 256 workgroups (two tiles for some)
