@@ -1038,6 +1038,7 @@ extern "C" int64_t selunet_gemm_stats_rows(const selunet_gather* a, int32_t n_co
   if (make_gather(a, dtype, g, 16 / esz)) return -1;
   if (halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype)) return conv3x3_halo_stats_rows(g, n_cols, dtype);
   // the bf16 ConvTranspose2d data gradient (BN-backward sums): the resident-weight kernel's rows
+  if (dtype == SELUNET_BF16 && convt_ring_bf16_dgrad_operand_ok(g, n_cols)) return convt_ring_rows(g, n_cols);
   if (dtype == SELUNET_BF16 && convt_dgrad_bf16_ntb(g, n_cols) > 0) return convt_dgrad_bf16_rows(g, n_cols);
   return gather_rows(g, n_cols);
 }
@@ -1117,7 +1118,8 @@ extern "C" int selunet_gemm_gather(const selunet_gather* a, const void* b, int32
   hipStream_t st = as_stream(stream);
   if (ep->mode != SELUNET_EP_SCATTER2X && halo_enabled() && conv3x3_halo_eligible(g, n_cols, dtype))
     return conv3x3_halo_launch(g, b, n_cols, k_pad, e, dtype, st);
-  if (dtype == SELUNET_BF16) {  // ConvTranspose2d forward / data gradient: the resident-weight kernels
+  if (dtype == SELUNET_BF16) {  // ConvTranspose2d forward / data gradient: the ring (unpool3 / 2) or resident kernels
+    if (convt_ring_bf16_takes(g, n_cols, e)) return convt_ring_bf16_launch(g, b, n_cols, e, st);
     if (convt_bf16_eligible(g, n_cols, e) || convt_dgrad_bf16_eligible(g, n_cols, e))
       return convt_bf16_launch(g, b, n_cols, e, st);
     SELUNET_REQUIRE(convt_dgrad_bf16_ntb(g, n_cols) == 0 || (e.stats == nullptr && e.colsum == nullptr &&

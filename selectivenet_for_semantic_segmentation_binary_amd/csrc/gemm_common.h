@@ -475,6 +475,9 @@ int64_t convt_ring_rows(const GatherArg& g, int N);
 bool convt_ring_x2_takes(const GatherArg& g, int N, const EpiArg& e);
 int convt_ring_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                          hipStream_t st);
+bool convt_ring_bf16_dgrad_operand_ok(const GatherArg& g, int N);
+bool convt_ring_bf16_takes(const GatherArg& g, int N, const EpiArg& e);
+int convt_ring_bf16_launch(const GatherArg& g, const void* w, int N, const EpiArg& e, hipStream_t st);
 int convt_bf16_fwd_ntb(const GatherArg& g, int N);  // bf16 resident-weight ConvTranspose2d (convt_bf16.hip)
 int convt_dgrad_bf16_ntb(const GatherArg& g, int N);
 int64_t convt_dgrad_bf16_rows(const GatherArg& g, int N);
