@@ -66,10 +66,10 @@ enum {
   SELUNET_OPT_WGRAD_BN_BI,        /* column tile of the BN-fused split-fp16 weight gradient for outputs of 128+
                                    * channels: 128 (0, default) or 64 (1: no half-tile staging, two k-steps of load
                                    * cover); selunet_conv3x3_wgrad_x2_ws_bytes sizes for either */
-  SELUNET_OPT_CONVT_RING,         /* fp32 ConvTranspose2d forward / data gradient with K >= 256 on 256-column blocks:
-                                   * the LDS-DMA ring kernel with the forward on 8 x 1 waves (2, default) or 4 x 2
-                                   * waves (1), or the resident-weight / staged kernels (0);
-                                   * selunet_gemm_gather_x2_stats_rows follows it */
+  SELUNET_OPT_CONVT_RING,         /* ConvTranspose2d forward / data gradient on 256-column blocks (fp32: K >= 256;
+                                   * bf16: K >= 512): the LDS-DMA ring kernels with the forward on 8 x 1 waves (2,
+                                   * default) or, fp32, 4 x 2 waves (1), or the resident-weight / staged kernels (0);
+                                   * selunet_gemm_gather_x2_stats_rows / selunet_gemm_stats_rows follow it */
   SELUNET_OPT_COUNT
 };
 /* Sets option `key` to `value` (< 0: default); returns the previous setting, or INT64_MIN for an
