@@ -581,6 +581,22 @@ def main():
             os.environ.pop("SELUNET_X2", None)
     if args.dtype == "fp32" and not args.no_bf16:
         extra = run_config(args, "bf16", world, rank, dev, xt, lt, hi - lo)
+    nosel = None
+    if args.dtype == "fp32" and not args.no_bf16 and args.selective:
+        # BASELINE configs[1]: UNet_B --selective 0 (the plain model, BCEWithLogits on its one head,
+        # train.py:194-209 with selective off), the same global batch, bf16 — timed like the headline
+        import copy
+        a = copy.copy(args)
+        a.selective = 0
+        a.no_full_loop = a.no_input_loop = True
+        nosel = run_config(a, "bf16", world, rank, dev, xt, lt, hi - lo)
+        nosel["config"] = {"workload": f"UNet_B (selective 0) train step, global bs={args.batch}, "
+                                       f"{args.size}x{args.size}, BCEWithLogits, Adam lr=1e-3",
+                           "model": "UNet_B", "global_batch": args.batch, "per_gpu_batch": hi - lo,
+                           "image": args.size, "parallelism": f"dp{world}"}
+        nosel["unit"] = "images/s"
+        nosel["note"] = ("BASELINE configs[1]: bf16 operands, fp32 accumulation and statistics; parity: "
+                         "step_nosel_n128_256.npz [bf16] (tests/test_gpu_fullsize.py)")
     size512 = None
     if not args.no_size512 and (args.size, args.batch) == (256, 128):
         size512 = run_size512(args, world, rank, dev)
@@ -646,6 +662,8 @@ def main():
             extra["step_mfma_frac"] = round(wb / world / PEAK["bf16"][0], 4)
             extra["note"] = "bf16 speed configuration (bf16 operands, fp32 accumulation); parity gates in DESIGN.md §4"
             line["bf16"] = extra
+        if nosel is not None:
+            line["bf16_nosel"] = nosel
         print(json.dumps(line))
     if world > 1:
         dist.barrier()

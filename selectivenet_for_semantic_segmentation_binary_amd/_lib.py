@@ -220,8 +220,10 @@ def load(auto_build: bool = False):
         path = lib_path()
         tree = _build.source_fingerprint()
         own = "SELUNET_LIB" not in os.environ
-        if auto_build and own and (not os.path.exists(path) or _build.lib_stamp_fingerprint(path) != tree):
-            _build.build(verbose=False)  # missing or stale: rebuild before the library is mapped
+        if auto_build and own and (not os.path.exists(path) or _build.lib_stamp(path) != _build.build_id(tree)):
+            # missing, stale or built for another arch: rebuild before the library is mapped (build() holds a
+            # file lock, so the ranks of one node build once)
+            _build.build(verbose=False)
         if not os.path.exists(path):
             raise RuntimeError(
                 f"{path} not found: the MI355X kernels are not built (run "

@@ -71,9 +71,15 @@ def parse_build_id(bid: str) -> tuple[str, str]:
 
 def lib_stamp_fingerprint(lib: str = None) -> str | None:
     """Source fingerprint recorded next to a built library (its .sha stamp), or None."""
+    bid = lib_stamp(lib)
+    return parse_build_id(bid)[0] if bid else None
+
+
+def lib_stamp(lib: str = None) -> str | None:
+    """The full build id ('<fingerprint> <arch>') recorded next to a built library, or None."""
     try:
         with open((lib or LIB) + ".sha") as f:
-            return parse_build_id(f.read())[0]
+            return f.read().strip()
     except OSError:
         return None
 
@@ -90,17 +96,33 @@ def _compile(path, obj, want, force):
     stamp = obj + ".sha"
     if not force and os.path.exists(obj) and _stamp_ok(stamp, want):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", path, "-o", obj]
+    tmp = f"{obj}.{os.getpid()}.tmp"
+    cmd = [HIPCC, *FLAGS, "-c", path, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {os.path.basename(path)}:\n{r.stderr[-6000:]}")
+    os.replace(tmp, obj)
     with open(stamp, "w") as f:
         f.write(want)
     return obj
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile and link under an exclusive file lock (several ranks of one node may call it at once
+    through load(auto_build=True): the first builds, the others wait and find the stamp current); the
+    library is linked to a temporary path and renamed into place, so a process that already mapped the
+    old file keeps a consistent image."""
+    import fcntl
     os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(force, verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(force, verbose):
     srcs = _sources()
     heads = _headers()
     fp = build_id()
@@ -117,10 +139,12 @@ def build(force: bool = False, verbose: bool = True) -> str:
         objs = list(ex.map(lambda j: _compile(*j, force), jobs))
     lib_stamp = LIB + ".sha"
     if force or not os.path.exists(LIB) or not _stamp_ok(lib_stamp, fp):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+        tmp = f"{LIB}.{os.getpid()}.tmp"
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        os.replace(tmp, LIB)
         with open(lib_stamp, "w") as f:
             f.write(fp)
     if verbose:

@@ -36,6 +36,8 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // selunet_set_option: the library reads no environment variables. Values < 0 mean "default".
 extern int64_t g_options[SELUNET_OPT_COUNT];
 inline int64_t option(int key, int64_t dflt) { return g_options[key] < 0 ? dflt : g_options[key]; }
+// allocates the SELUNET_OPT_TILE_QUEUE ticket counters on the current device (conv3x3.hip); 0 on success
+int x2_tile_queue_prepare();
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -2474,15 +2474,35 @@ bool conv3x3_x2_eligible(const GatherArg& g, int N) {
 // (conv3x3_halo_persist_kernel, TQ) and flushes statistics per tile (slab rows = pixel tiles)
 bool x2_tile_queue() { return option(SELUNET_OPT_TILE_QUEUE, 0) != 0; }
 
-// the queue's counters: [2][n_tiles <= 64], zero between launches (each launch's last workgroups reset them);
-// allocated on first use on the current device (one process per GPU)
-static unsigned* tq_counters() {
-  static unsigned* p = nullptr;
-  if (p == nullptr) {
-    if (hipMalloc(&p, 128 * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, 128 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+// the queue's counters: [2][n_tiles <= 64] per device, zero between launches (each launch's last workgroups
+// reset them). Allocated by selunet_set_option(SELUNET_OPT_TILE_QUEUE, > 0) on the current device — outside
+// any stream capture — or on first use when the launch stream is not capturing. One launch in flight per
+// device: the engine issues the persistent convolutions on one compute stream, so launches never overlap.
+static unsigned* g_tq[64] = {};
+
+int x2_tile_queue_prepare() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+  if (g_tq[dev] != nullptr) return 0;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, 128 * sizeof(unsigned)) != hipSuccess) return -1;
+  if (hipMemset(p, 0, 128 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return -1;
   }
-  return p;
+  g_tq[dev] = p;
+  return 0;
+}
+
+static unsigned* tq_counters(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (g_tq[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (x2_tile_queue_prepare() != 0) return nullptr;
+  }
+  return g_tq[dev];
 }
 
 // statistics slab rows of selunet_conv3x3_x2 (persistent kernel): workgroups per column tile, or pixel tiles
@@ -2500,8 +2520,10 @@ static int launch_x2(const GatherArg& g, const float* w, int N, const EpiArg& ep
   // 16x16x32 MFMAs at BN = 64 (1-4 % faster per layer); at BN = 128 they cost 20-25 % (the extra
   // fragment registers spill: 180 B of scratch per lane against 44) — DESIGN.md §3
   if (x2_tile_queue()) {
-    unsigned* tq = tq_counters();
-    if (tq == nullptr || n_tiles > 64) return fail(SELUNET_ELAUNCH, "conv3x3_x2: tile-queue counters unavailable");
+    unsigned* tq = tq_counters(st);
+    if (tq == nullptr || n_tiles > 64)
+      return fail(SELUNET_ELAUNCH, "conv3x3_x2: tile-queue counters unavailable (set SELUNET_OPT_TILE_QUEUE "
+                                   "before capturing the step)");
     hipLaunchKernelGGL((conv3x3_halo_persist_kernel<float, BN, true, BN == 64, true>), dim3((unsigned)(gp * n_tiles)),
                        dim3(HTHREADS), 0, st, g, w, N, k_pad, ep, n_tiles, tiles_x, tiles_y,
                        (int)conv3x3_halo_tiles(g), gp, w + (int64_t)N * k_pad, amax0, amax1, tq);

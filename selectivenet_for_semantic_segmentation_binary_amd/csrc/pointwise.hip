@@ -1608,6 +1608,10 @@ int64_t selunet_set_option(int32_t key, int64_t value) {
     return INT64_MIN;
   }
   const int64_t prev = g_options[key];
+  if (key == SELUNET_OPT_TILE_QUEUE && value > 0 && x2_tile_queue_prepare() != 0) {
+    set_error("selunet_set_option: tile-queue counters could not be allocated on the current device");
+    return INT64_MIN;
+  }
   g_options[key] = value < 0 ? -1 : value;
   return prev;
 }

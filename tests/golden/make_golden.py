@@ -424,7 +424,7 @@ def kats():
 
 
 def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, epochs=5, lamb=2, seed=0, member=0,
-                 hard=None, cosine_min=None):
+                 hard=None, cosine_min=None, conv_noise=0, conv_eps=3e-7):
     """mIoU parity run (BASELINE.json 'mIoU parity'): the reference training loop
     (train.py:183-241: forward, BCEWithLogits aux + calc_selective_risk_image_b, Adam, the
     per-batch Evaluator on the fp64-sigmoid masks) for `epochs` passes over a seeded synthetic
@@ -448,6 +448,11 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
         xtr = _perturbed(xtr, member)
     torch.manual_seed(0)
     net = build_ref(seed, True)
+    # conv-noise member: every Conv2d / ConvTranspose2d output of every training forward
+    # carries a fresh (1 + conv_eps * N(0, 1)) rounding-level perturbation — a model of another fp32 summation
+    # order through all 128 steps, not only of the input; removed before the eval pass (the eval forward of a
+    # different implementation rounds too, but its masks are compared within the measured logit error elsewhere)
+    hooks = _conv_noise_hooks(net, conv_eps, conv_noise) if conv_noise else []
     optim = torch.optim.Adam(net.parameters(), lr=1e-3)
     # --lr_sche CosineAnnealingLR --patience <epochs> --lr_min <cosine_min> (train.py:100-101, stepped once
     # per epoch at train.py:246-250)
@@ -481,6 +486,8 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
            "meta_lamb": lamb, "meta_seed": seed, "meta_train_seed": 2024, "meta_val_seed": 2025,
            "train_losses": np.array(losses), "train_cm": ev.confusion_matrix.copy(),
            "train_selected": np.int64(total - reject), "train_total": np.int64(total)}
+    for h in hooks:
+        h.remove()
     net.eval()
     evs, evp = Evaluator(num_class=2, selective=True), Evaluator(num_class=2, selective=False)
     vlosses, vsel = [], 0
@@ -499,7 +506,7 @@ def miou_fixture(fname="miou_sel_64.npz", n_train=64, n_val=32, size=64, bs=8, e
     out.update({"val_losses": np.array(vlosses), "val_cm_selective": evs.confusion_matrix.copy(),
                 "val_cm": evp.confusion_matrix.copy(), "val_miou_selective": np.float64(evs.get_mIoU()),
                 "val_miou": np.float64(evp.get_mIoU()), "val_selected": np.int64(vsel)})
-    if member:
+    if member or conv_noise:
         return out
     path = os.path.join(HERE, fname)
     np.savez_compressed(path, **out)
@@ -615,37 +622,42 @@ MIOU256S = dict(fname="miou_sel_256s.npz", n_train=128, n_val=256, size=256, bs=
 MIOU_SETS = {"h": MIOU256H, "s": MIOU256S}
 
 
-def miou_member_path(tag, k):
-    return os.path.join(HERE, f"_miou256{tag}_member{k}.npz")
+def miou_member_path(tag, k, conv=False):
+    return os.path.join(HERE, f"_miou256{tag}_{'c' if conv else ''}member{k}.npz")
 
 
-def miou_collect_ens(tag, members):
+def miou_collect_ens(tag, members, conv=False):
     """Fold the members written by `miou256x_member <tag> k` into fixture MIOU_SETS[tag]: the
     ensemble arrays (validation / selective / training-phase mIoU, selected-pixel counts and selective
-    confusion matrices per member) are extended by the new members (members already present stay)."""
+    confusion matrices per member) are extended by the new members (members already present stay).
+    conv=True folds `miou256c_member` runs (conv-output noise) into the `*_cens` arrays instead."""
     cfg = MIOU_SETS[tag]
     path = os.path.join(HERE, cfg["fname"])
     d = dict(np.load(path, allow_pickle=False))
-    have = [int(v) for v in d.get("ens_members", np.arange(1, len(d.get("val_miou_ens", [])) + 1))]
-    keys = ("val_miou_ens", "val_miou_selective_ens", "train_miou_ens", "val_selected_ens", "val_cm_selective_ens")
+    sfx, mkey = ("_cens", "ens_cmembers") if conv else ("_ens", "ens_members")
+    have = [int(v) for v in d.get(mkey, np.arange(1, len(d.get("val_miou" + sfx, [])) + 1))]
+    keys = tuple(k + sfx for k in ("val_miou", "val_miou_selective", "train_miou", "val_selected",
+                                   "val_cm_selective"))
     cur = {k: list(d[k]) if k in d else [] for k in keys}
     for k in members:
         if k in have:
             continue
-        r = dict(np.load(miou_member_path(tag, k), allow_pickle=False))
-        cur["val_miou_ens"].append(float(r["val_miou"]))
-        cur["val_miou_selective_ens"].append(float(r["val_miou_selective"]))
-        cur["train_miou_ens"].append(_miou_cm(r["train_cm"]))
-        cur["val_selected_ens"].append(int(r["val_selected"]))
-        cur["val_cm_selective_ens"].append(np.asarray(r["val_cm_selective"], np.float64))
+        r = dict(np.load(miou_member_path(tag, k, conv), allow_pickle=False))
+        cur["val_miou" + sfx].append(float(r["val_miou"]))
+        cur["val_miou_selective" + sfx].append(float(r["val_miou_selective"]))
+        cur["train_miou" + sfx].append(_miou_cm(r["train_cm"]))
+        cur["val_selected" + sfx].append(int(r["val_selected"]))
+        cur["val_cm_selective" + sfx].append(np.asarray(r["val_cm_selective"], np.float64))
         have.append(k)
     for k in keys:
         if cur[k]:
             d[k] = np.array(cur[k])
-    d["ens_members"] = np.array(have, np.int64)
+    d[mkey] = np.array(have, np.int64)
+    if conv:
+        d["meta_cens_eps"] = np.float64(3e-7)
     np.savez_compressed(path, **d)
-    sp = np.abs(d["val_miou_ens"] - float(d["val_miou"])).max()
-    sps = np.abs(d["val_miou_selective_ens"] - float(d["val_miou_selective"])).max()
+    sp = np.abs(d["val_miou" + sfx] - float(d["val_miou"])).max()
+    sps = np.abs(d["val_miou_selective" + sfx] - float(d["val_miou_selective"])).max()
     print(f"wrote {path}: {len(have)} members, spread val {sp:.5f} selective {sps:.5f} "
           f"(val {float(d['val_miou']):.5f}, selective {float(d['val_miou_selective']):.5f})")
 
@@ -1059,6 +1071,17 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:2] == ["miou256x_collect"]:  # miou256x_collect <h|s> k1 k2 ...
         miou_collect_ens(sys.argv[2], [int(v) for v in sys.argv[3:]])
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256c_member"]:  # miou256c_member <h|s> k: one conv-output-noise member (3e-7)
+        tag, k = sys.argv[2], int(sys.argv[3])
+        r = miou_fixture(conv_noise=k, **MIOU_SETS[tag])
+        np.savez(miou_member_path(tag, k, conv=True), **r)
+        print(f"conv-noise member {tag}{k}: val mIoU {float(r['val_miou']):.5f} selective "
+              f"{float(r['val_miou_selective']):.5f} train {_miou_cm(r['train_cm']):.5f} "
+              f"selected {int(r['val_selected'])}", flush=True)
+        sys.exit(0)
+    if sys.argv[1:2] == ["miou256c_collect"]:  # miou256c_collect <h|s> k1 k2 ...
+        miou_collect_ens(sys.argv[2], [int(v) for v in sys.argv[3:]], conv=True)
         sys.exit(0)
     if sys.argv[1:2] == ["miou256h_collect"]:
         miou_collect(int(sys.argv[2]) if len(sys.argv) > 2 else 8, MIOU256H["fname"])

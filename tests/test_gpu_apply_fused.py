@@ -400,3 +400,37 @@ def test_wgrad_x2_bn_src_argument_checks():
     with pytest.raises(K.SelunetError):
         K.call("selunet_conv3x3_wgrad_x2_bn_src", K.gather(n, h, w, 1, K.source(y, 64)), gq, K.ptr(ws), ws.numel() * 4,
                K.ptr(out), K.ptr(xw), K.ptr(xw), None, bnb, K.ptr(coef), bad, None, None, K.stream_ptr())
+
+
+@pytest.mark.parametrize("n,size", [(4, 64), (2, 128)])
+def test_step_fused_applies_on_off(monkeypatch, n, size):
+    """Step-level check of the fused BN-backward applies: one fp32 training step with the
+    applies fused into the split-fp16 weight gradients (SELUNET_FUSE_WGRAD_APPLY / _SRC = 1, default)
+    against the same step with every apply standalone (= 0). The data gradients see bit-identical dy, so
+    the loss and outputs are equal and every gradient agrees within split-fp16 rounding (the fused weight
+    gradients split dy under the finalize's analytic |dy| bound instead of its exact max). At 64x64 the
+    8x8 bottleneck layers run on the gather GEMM, whose epilogue must still write the max |dA| word the
+    fused consumer's bound starts from — a missing word would leave k0 |dA| out of the bound."""
+    import numpy as np
+    from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
+    import selectivenet_for_semantic_segmentation_binary_amd as S
+    from tests.test_gpu_model import build, train_step
+    x, lab = make_batch(n, size, seed=4)
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SELUNET_FUSE_WGRAD_APPLY", fused)
+        monkeypatch.setenv("SELUNET_FUSE_WGRAD_SRC", fused)
+        net = build(True)
+        opt = S.Adam(net.parameters(), lr=1e-3)
+        res.append([train_step(net, opt, xt, lt, True, 2) for _ in range(2)])
+    (a0, a1), (b0, b1) = res
+    assert a0["loss"] == b0["loss"] and np.array_equal(a0["output"], b0["output"])
+    worst = 0.0
+    for k in a0["grads"]:
+        ga, gb = a0["grads"][k].astype(np.float64), b0["grads"][k].astype(np.float64)
+        e = np.linalg.norm(ga - gb) / max(np.linalg.norm(gb), 1e-30)
+        worst = max(worst, e)
+        assert e <= 1e-5, (k, e)
+    assert abs(a1["loss"] - b1["loss"]) <= 1e-5 * abs(b1["loss"]), (a1["loss"], b1["loss"])
+    print(f"fused vs unfused applies at {n}x{size}^2: worst gradient rel L2 {worst:.2e}")
