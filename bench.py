@@ -95,7 +95,6 @@ class KernelTimer:
     HBM bytes (each operand tensor read once, each output written once) and its bound."""
 
     MFMA = ("selunet_gemm_gather", "selunet_gemm_gather_x2", "selunet_conv3x3_wino", "selunet_conv3x3_x2",
-            "selunet_conv3x3_wx2",
             "selunet_conv3x3_wgrad_x2", "selunet_conv3x3_wgrad_x2_bn", "selunet_conv3x3_wgrad_x2_bn_src",
             "selunet_gemm_wgrad_x2",
             "selunet_gemm_wgrad", "selunet_gemm_wgrad_ws", "selunet_gemm_wgrad_ws_to")
@@ -156,15 +155,6 @@ class KernelTimer:
             flops = 3 * 2.0 * m * n_cols * self._k(g)
             nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * self._k(g) * esz
             return kname, "mfma_f16", flops, nbytes, f"x2 {g.h}x{g.w} K={self._k(g)} N={n_cols} mode={ep.mode}"
-        if name == "selunet_conv3x3_wx2":  # (g, w, n_cols, ep, amax0, amax1, stream): split-fp16 Winograd F(2,3)
-            g, n_cols = args[0], _i(args[2])
-            m = g.n * g.h * g.w
-            c = self._k(g) // 9
-            # executed fp16 MFMA work: three products per fp32 product, 6 products per pixel and
-            # channel (4 per output pair and kernel row) instead of the direct form's 9
-            flops = 3 * 2.0 * m * n_cols * 6 * c
-            nbytes = self._src_bytes(g) + m * n_cols * esz + n_cols * 12 * c * esz
-            return "conv3x3_wx2<f32,128>", "mfma_f16", flops, nbytes, f"wx2 {g.h}x{g.w} C={c} N={n_cols}"
         if name == "selunet_conv3x3_wgrad_x2":  # (gp, gq, ws, wsb, out, amax_p, amax_q0, amax_q1, stream)
             gp, gq = args[0], args[1]
             kname = f"conv3x3_wgrad_x2<{128 if self._k(gp) % 128 == 0 else 64}>+reduce"

@@ -42,7 +42,7 @@ enum {
  * variables; every value < 0 selects the built-in default. Selection options take 0/1. */
 enum {
   SELUNET_OPT_HALO = 0,           /* 3x3 convolutions on the LDS halo kernels (1) or the gather GEMM (0) */
-  SELUNET_OPT_HALO_PERSIST,       /* persistent halo kernel: 0 off, 1 multi-chunk layers, 2 single-chunk too (1) */
+  SELUNET_OPT_HALO_PERSIST,       /* persistent halo kernel for multi-chunk layers: 0 off, 1 on (1) */
   SELUNET_OPT_WINO,               /* exact-fp32 3x3 fwd/dgrad as 1-D Winograd F(2,3) (1) or direct (0) */
   SELUNET_OPT_WINO_WGRAD,         /* exact-fp32 3x3 weight gradient as the Winograd transpose (1) */
   SELUNET_OPT_WINO_WGRAD_TW,      /* its tile width: 16 (default) or 8 pixels */
@@ -54,18 +54,12 @@ enum {
   SELUNET_OPT_RF_SINGLE,          /* slab rows reduced in one launch by the fused reductions (1024) */
   SELUNET_OPT_APPLY_U8,           /* BN-backward apply form: 0 8 ch x 4 px, 1 8 ch x 8 px, 2/3 4 contiguous ch x 8/16 px (0) */
   SELUNET_OPT_APPLY_GRID,         /* BN-backward apply: grid cap (1024) */
-  SELUNET_OPT_WX2,                /* selunet_conv3x3_wx2_ok admits layers to the split-fp16 Winograd kernel (0:
-                                   * measured slower than selunet_conv3x3_x2 on every UNet_B layer) */
   SELUNET_OPT_X2D,                /* 64-column split-fp16 3x3 layers on the two-workgroups-per-CU kernel: 0 never,
                                    * 1 every eligible layer, 2 inputs of at most 64 channels, 3 (default) those of
                                    * them whose source carries a BN+ReLU transform (the forwards) */
-  SELUNET_OPT_BF16_M16,           /* bf16 persistent 3x3 kernel on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0) */
   SELUNET_OPT_TILE_QUEUE,         /* split-fp16 persistent 3x3 kernel: pixel tiles from a ticket counter, statistics
                                    * per tile (1), or the static walk (0, default); selunet_conv3x3_x2_stats_rows
                                    * follows it (robustness to a concurrent all-reduce) */
-  SELUNET_OPT_WGRAD_BN_BI,        /* column tile of the BN-fused split-fp16 weight gradient for outputs of 128+
-                                   * channels: 128 (0, default) or 64 (1: no half-tile staging, two k-steps of load
-                                   * cover); selunet_conv3x3_wgrad_x2_ws_bytes sizes for either */
   SELUNET_OPT_CONVT_RING,         /* ConvTranspose2d forward / data gradient on 256-column blocks (fp32: K >= 256;
                                    * bf16: K >= 512): the LDS-DMA ring kernels with the forward on 8 x 1 waves (2,
                                    * default) or, fp32, 4 x 2 waves (1), or the resident-weight / staged kernels (0);
@@ -264,23 +258,10 @@ int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32_t n_cols, 
                        const float* amax0, const float* amax1, void* stream);
 const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, int32_t n_cols, int32_t mode, int32_t split);
 /* Statistics slab rows (stats / colsum / BN-backward sums of the epilogue) selunet_conv3x3_x2 and
- * selunet_conv3x3_wx2 write for this operand: the layers SELUNET_OPT_X2D sends to the 64-column kernel
+ * write for this operand: the layers SELUNET_OPT_X2D sends to the 64-column kernel
  * with two 256-thread workgroups per CU have min(16x16 tiles, 512) rows, others as
  * selunet_gemm_stats_rows. selunet_conv3x3_x2_kernel_name names the kernel a call would run. */
 int64_t selunet_conv3x3_x2_stats_rows(const selunet_gather* a, int32_t n_cols);
-/* The same fp32 3x3 conv forward / data gradient on split-fp16 operands as a 1-D Winograd F(2,3) along
- * x (model.py:11): per kernel row dy and output pair (x, x+1), M_xi = sum_c U_xi[c] * V_xi[c] over
- * V = (d0 - d2, d1 + d2, d2 - d1, d1 - d3) of the four inputs x-1..x+2 (formed in fp32 from the
- * BN+ReLU-transformed source, then split) and U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2) of the kernel
- * row (fp64, rounded once, then split); y(x) = (M0 + M1) + M2, y(x+1) = (M1 - M2) - M3. Four fp16
- * products per output pair and kernel row instead of six: 2/3 of selunet_conv3x3_x2's MFMAs. w: a
- * SELUNET_PACK_CONV3X3_WX2 pack. Same gathers, range words, epilogues and statistics slab rows as
- * selunet_conv3x3_x2; selunet_conv3x3_wx2_ok tells whether a layer should take it (SELUNET_OPT_WX2 set, and
- * h, w >= 16, w even, C and c_src0 multiples of 16, 64 <= C <= 512, n_cols a multiple of 64). At bs=128 it
- * measured 5-35 % slower than selunet_conv3x3_x2 per layer, so the option is off by default. */
-int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols);
-int selunet_conv3x3_wx2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
-                        const float* amax0, const float* amax1, void* stream);
 /* Range word of a training-mode BatchNorm+ReLU output relu(gamma*xhat + beta) over `count` values
  * per channel: |xhat| <= sqrt(count - 1) for batch statistics (Samuelson's inequality), so
  * *out = max_c |gamma_c| * sqrt(count) + max_c |beta_c| bounds every element (max-pooled copies
@@ -343,13 +324,6 @@ int32_t selunet_wgrad_ld(int32_t kq);
  * matrix: fwd + co*9*ci (co floats), dgrad + ci*9*co (ci floats). ci, co multiples of 32. */
 /* SELUNET_PACK_CONVT_X2 (fp32): the same split-fp16 format for a ConvTranspose2d weight [ci][co][2][2]:
  * fwd = [4*co][ci] (row (a*2+b)*co + o, k_pad = ci) + 4*co unscale factors, dgrad = [ci][4*co] + ci. */
-/* SELUNET_PACK_CONV3X3_WX2 (fp32): split-fp16 Winograd operands of selunet_conv3x3_wx2, k_pad = 12*ci;
- * fwd = [co][12*ci] and dgrad = [ci][12*co] 32-bit words (dgrad from the flipped / transposed kernel):
- * the U values of row r (output channel o for fwd, input channel c for dgrad) over the k channels in
- * blocks ((k / 16) * 3 + dy) * 4 + q of 16 channels (q = 0, 2, 1, 3 for xi = 0, 1, 2, 3), each block
- * stored as 16 fp16 high parts then 16
- * low parts, the row scaled by 2^e_row (max|U_row| * 2^e_row < 2^14); the row unscale factors follow
- * the matrix as for SELUNET_PACK_CONV3X3_X2. ci, co multiples of 16, at most 512. */
 /* SELUNET_PACK_COPY (any dtype): co*ci fp32 values w -> fwd unchanged (dgrad unused) — the heads'
  * current weights and biases (model.py:62,65,66) gathered into the contiguous [heads][64] / [heads]
  * operands of selunet_heads_fwd in the same launch. */
@@ -359,8 +333,7 @@ enum {
   SELUNET_PACK_CONV3X3_WINO = 2,
   SELUNET_PACK_CONV3X3_X2 = 3,
   SELUNET_PACK_CONVT_X2 = 4,
-  SELUNET_PACK_COPY = 5,
-  SELUNET_PACK_CONV3X3_WX2 = 6
+  SELUNET_PACK_COPY = 5
 };
 typedef struct selunet_pack_desc {
   const float* w;

@@ -57,7 +57,6 @@ class PackDesc(ctypes.Structure):
 
 
 PACK_MAX, PACK_CONV3X3, PACK_CONVT, PACK_CONV3X3_WINO, PACK_CONV3X3_X2, PACK_CONVT_X2, PACK_COPY = 32, 0, 1, 2, 3, 4, 5
-PACK_CONV3X3_WX2 = 6
 WG_CONV3X3, WG_CONVT = 1, 2  # selunet_gemm_wgrad_ws_to layouts
 
 
@@ -101,9 +100,7 @@ SIGNATURES = {
                                          P]),
     "selunet_conv3x3_x2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
     "selunet_conv3x3_x2_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(Gather), c_int32, c_int32, c_int32]),
-    "selunet_conv3x3_wx2_ok": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "selunet_conv3x3_x2_stats_rows": (c_int64, [ctypes.POINTER(Gather), c_int32]),
-    "selunet_conv3x3_wx2": (c_int32, [ctypes.POINTER(Gather), P, c_int32, ctypes.POINTER(Epilogue), P, P, P]),
     "selunet_act_bound": (c_int32, [P, P, c_int32, c_int64, P, P]),
     "selunet_conv3x3_wgrad_x2_ws_bytes": (c_int64, [ctypes.POINTER(Gather), ctypes.POINTER(Gather)]),
     "selunet_gemm_wgrad_x2_ws_bytes": (c_int64, [ctypes.POINTER(Gather), ctypes.POINTER(Gather)]),
@@ -253,8 +250,8 @@ def load(auto_build: bool = False):
 # selunet_option keys (include/selunet.h)
 OPT = {name: i for i, name in enumerate([
     "HALO", "HALO_PERSIST", "WINO", "WINO_WGRAD", "WINO_WGRAD_TW", "WINO_WGRAD_WAVES", "WGRAD_WGS",
-    "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "WX2", "X2D",
-    "BF16_M16", "TILE_QUEUE", "WGRAD_BN_BI", "CONVT_RING"])}
+    "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "X2D",
+    "TILE_QUEUE", "CONVT_RING"])}
 # environment variables the host maps onto options at load (A/B and ablation runs of tools/ and the
 # exact-fp32 comparison paths of the tests); SELUNET_NO_HALO=1 means HALO=0
 ENV_OPTIONS = {f"SELUNET_{k}": v for k, v in OPT.items() if k != "HALO"}

@@ -313,7 +313,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
                             unsigned* __restrict__ tq = nullptr) {
   static_assert(!TQ || X2, "tile queue: split-fp16 kernel only");
   static_assert(!X2 || std::is_same<T, float>::value, "split-fp16 form of fp32 operands only");
-  static_assert(!M16 || X2 || std::is_same<T, __bf16>::value, "16x16x32 form: split-fp16 or bf16");
+  static_assert(!M16 || X2, "16x16x32 form: split-fp16 only (the bf16 form lost every A/B, retired in round 6)");
   constexpr int E = 16 / sizeof(T);
   constexpr int CK = 128 / sizeof(T);
   constexpr int WAVES_N = BN / 64;
@@ -478,26 +478,7 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     const unsigned char* b_src = Bs + bbuf * BN * WROWB;
     const int dy = t / 3, dx = t - (t / 3) * 3;
     const int tap_off = dy * HWT + dx;
-    if constexpr (M16 && !X2) {
-      // bf16: a tap's 64-channel chunk as two 16x16x32 k-steps (16-B units 0-3, 4-7 of the 128-B rows);
-      // per k-step the wave's 4 column subtiles' weight fragments, then per tile row its halo fragment
-      // and 4 MFMAs (unit ^ halo-row parity undoes the halo swizzle of halo_store)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 bw[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          bw[b] = *reinterpret_cast<const bf16x8*>(b_src + (wn * 64 + b * 16 + l16) * WROWB + (ks * 4 + kg) * 16);
-#pragma unroll
-        for (int a = 0; a < RT; ++a) {
-          const int py = wm * RT + a;
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-              a_src + ((py + dy) * HWT + l16 + dx) * AROWB + (((ks * 4 + kg) ^ ((py + dy) & 1)) << 4));
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[b], acc[a][b], 0, 0, 0);
-        }
-      }
-    } else if constexpr (M16) {
+    if constexpr (M16) {
       // the wave's 4 column subtiles' weight fragments (high, low), then per tile row its halo
       // fragments and 12 MFMAs; unit kg ^ (halo row parity) undoes the halo swizzle (halo_store)
       f16x8 bh[4], bl[4];
@@ -2260,10 +2241,9 @@ int conv3x3_wgrad_wino_launch(const GatherArg& p, const GatherArg& q, float* ws,
   return check_launch("conv3x3_wgrad_wino");
 }
 
-// column tile of the split-fp16 weight gradient (bn: the BN-fused form, SELUNET_OPT_WGRAD_BN_BI)
-int conv3x3_wgrad_x2_bi(const GatherArg& p, bool bn) {
-  return p.K % 128 == 0 && !(bn && option(SELUNET_OPT_WGRAD_BN_BI, 0) == 1) ? 128 : 64;
-}
+// column tile of the split-fp16 weight gradient (plain and BN-fused forms alike; 64-column tiles for the fused
+// 128+-channel layers measured 4 % slower, profiles/r05g_wgrad_bn_bi64_ab.txt)
+int conv3x3_wgrad_x2_bi(const GatherArg& p, bool /*bn*/) { return p.K % 128 == 0 ? 128 : 64; }
 
 // pixel-tile splits of the split-fp16 weight gradient: ~256 workgroups over (co tile, ci chunk, split)
 int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t* per_out, bool bn) {
@@ -2381,11 +2361,9 @@ static int PERSIST_WGS = PERSIST_WGS_DEFAULT;  // selunet_set_halo_workgroups
 
 static bool persist_enabled() { return option(SELUNET_OPT_HALO_PERSIST, 1) != 0; }
 
-// single-chunk layers (C = one 128-B chunk) run the non-persistent ONE_CHUNK kernel (two workgroups per CU),
-// unless SELUNET_OPT_HALO_PERSIST = 2 puts them on the persistent kernel too
-static bool halo_one_chunk(const GatherArg& g, int dtype) {
-  return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64) && option(SELUNET_OPT_HALO_PERSIST, 1) != 2;
-}
+// single-chunk layers (C = one 128-B chunk) run the non-persistent ONE_CHUNK kernel (two workgroups per CU;
+// the persistent kernel measured 7 % slower on them, profiles/r04h_halo_persist_one_chunk.txt)
+static bool halo_one_chunk(const GatherArg& g, int dtype) { return g.Ctot == (dtype == SELUNET_F32 ? 32 : 64); }
 bool conv3x3_halo_one_chunk(const GatherArg& g, int dtype) { return halo_one_chunk(g, dtype); }
 
 // output tiles per workgroup row of the persistent launch (= statistics slab rows): PERSIST_WGS
@@ -2415,10 +2393,7 @@ static void launch_halo(const GatherArg& g, const void* b, int N, int k_pad, con
   const bool one = halo_one_chunk(g, dtype);
   if (!one && persist_enabled()) {
     const int gp = (int)conv3x3_halo_stats_rows(g, N, dtype);
-    // bf16: 16x16x32 MFMAs (SELUNET_OPT_BF16_M16; 160-B weight rows)
     auto k = conv3x3_halo_persist_kernel<T, BN, false>;
-    if constexpr (sizeof(T) == 2)
-      if (option(SELUNET_OPT_BF16_M16, 0) == 1) k = conv3x3_halo_persist_kernel<T, BN, false, true>;
     hipLaunchKernelGGL(k, dim3((unsigned)(gp * n_tiles)), dim3(HTHREADS), 0, st, g, reinterpret_cast<const T*>(b), N,
                        k_pad, ep, n_tiles, tiles_x, tiles_y, (int)conv3x3_halo_tiles(g), gp, nullptr, nullptr, nullptr,
                        nullptr);

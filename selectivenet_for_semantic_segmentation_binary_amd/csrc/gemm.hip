@@ -1262,33 +1262,6 @@ extern "C" int selunet_conv3x3_x2(const selunet_gather* a, const float* w, int32
   return conv3x3_x2_launch(g, w, n_cols, e, amax0, amax1, as_stream(stream));
 }
 
-extern "C" int32_t selunet_conv3x3_wx2_ok(int32_t h, int32_t w, int32_t c_in, int32_t c_src0, int32_t n_cols) {
-  if (x2_tile_queue()) return 0;  // the Winograd kernel keeps the static walk (its slab rows)
-  // (measured slower than selunet_conv3x3_x2 on every UNet_B layer: off unless SELUNET_OPT_WX2 = 1)
-  return option(SELUNET_OPT_WX2, 0) != 0 && halo_enabled() && conv3x3_x2_shape_ok(h, w, c_in, c_src0, n_cols) &&
-                 conv3x3_wx2_shape_ok(h, w, c_in, c_src0, n_cols)
-             ? 1
-             : 0;
-}
-
-extern "C" int selunet_conv3x3_wx2(const selunet_gather* a, const float* w, int32_t n_cols, const selunet_epilogue* ep,
-                                   const float* amax0, const float* amax1, void* stream) {
-  GatherArg g;
-  EpiArg e;
-  SELUNET_REQUIRE(a != nullptr && a->taps == 9, "conv3x3_wx2: a 3x3 (taps = 9) gather is required");
-  if (int rc = check_gather_call(a, w, n_cols, 9 * (a->src[0].channels + (a->nsrc > 1 ? a->src[1].channels : 0)), ep,
-                                 SELUNET_F32, g, e))
-    return rc;
-  SELUNET_REQUIRE(ep->mode != SELUNET_EP_SCATTER2X, "conv3x3_wx2: scatter epilogue not supported");
-  SELUNET_REQUIRE(amax0 != nullptr && (a->nsrc == 1 || amax1 != nullptr),
-                  "conv3x3_wx2: every source needs its range word (amax0, amax1)");
-  SELUNET_REQUIRE(halo_enabled() && conv3x3_x2_eligible(g, n_cols) &&
-                      conv3x3_wx2_shape_ok(g.h, g.w, g.Ctot, g.src[0].C, n_cols),
-                  "conv3x3_wx2: operand not eligible (%dx%d, C=%d, n_cols=%d; see selunet_conv3x3_wx2_ok)", g.h, g.w,
-                  g.Ctot, n_cols);
-  return conv3x3_wx2_launch(g, w, n_cols, e, amax0, amax1, as_stream(stream));
-}
-
 // Deterministic split reduction of the weight-gradient partials: out[i][j] = sum_s ws[s][i][j]
 // for j < kq (fixed split order), 0 in the pad columns. LAYOUT != PACKED writes the reference
 // parameter layout instead of the packed [ni][ldo] one (the unpack pass folded into the reduction):
@@ -1582,7 +1555,7 @@ static int plan_wgrad_x2(const selunet_gather* p, const selunet_gather* q, Wgrad
 }
 
 extern "C" int64_t selunet_conv3x3_wgrad_x2_ws_bytes(const selunet_gather* p, const selunet_gather* q) {
-  WgradPlan w, wb;  // (the plain and the BN-fused forms' splits may differ: SELUNET_OPT_WGRAD_BN_BI)
+  WgradPlan w, wb;  // (the plain and the BN-fused forms' split plans)
   if (plan_wgrad_x2(p, q, w) || plan_wgrad_x2(p, q, wb, true)) return -1;
   return std::max(w.splits, wb.splits) * (int64_t)w.ni * w.nj_pad * 4;
 }

@@ -486,10 +486,6 @@ bool convt_dgrad_bf16_eligible(const GatherArg& g, int N, const EpiArg& e);
 int convt_bf16_launch(const GatherArg& g, const void* w, int N, const EpiArg& e, hipStream_t st);
 int convt_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& e, const float* amax_src,
                     hipStream_t st);
-// the same on the split-fp16 1-D Winograd F(2,3) kernel (conv3x3_wx2.hip, selunet_conv3x3_wx2)
-bool conv3x3_wx2_shape_ok(int h, int w, int c_in, int c_src0, int n_cols);
-int conv3x3_wx2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
-                       const float* amax1, hipStream_t st);
 int64_t conv3x3_persist_rows(const GatherArg& g, int N);  // workgroup rows of the persistent 3x3 kernels
 int conv3x3_persist_wgs();  // their workgroup target (selunet_set_halo_workgroups; default 256 = one per CU)
 // the 64-column split-fp16 kernel, two 256-thread workgroups per CU (conv3x3_x2d.hip)

@@ -12,8 +12,8 @@ namespace selunet {
 // ------------------------------------------------------------------ error state, options
 static thread_local char g_err[512] = "";
 
-int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-static_assert(SELUNET_OPT_COUNT == 19, "g_options initialiser: one -1 per option");
+int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(SELUNET_OPT_COUNT == 16, "g_options initialiser: one -1 per option");
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -171,39 +171,18 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
   const selunet_pack_desc& d = l.d[t];
   const int co = d.co, ci = d.ci;
   const bool ct = d.kind == SELUNET_PACK_CONVT_X2;  // ConvTranspose2d [ci][co][2][2]
-  const bool wx = d.kind == SELUNET_PACK_CONV3X3_WX2;  // Winograd F(2,3) U values
   const int fwd_rows = ct ? 4 * co : co;
   const int r = (int)(b - d.offset);
   const bool fw = r < fwd_rows;
   const int row = fw ? r : r - fwd_rows;
-  const int len = ct ? (fw ? ci : 4 * co) : (fw ? (wx ? 12 : 9) * ci : (wx ? 12 : 9) * co);
+  const int len = ct ? (fw ? ci : 4 * co) : (fw ? 9 * ci : 9 * co);
   const float* w = d.w;
   // the row is gathered in SOURCE order (j walks the fp32 master's memory, contiguous runs of 9 taps
   // / 4 positions) into LDS at its packed position k, then max-reduced and written in k order
-  __shared__ float rowv[12 * 512];
+  __shared__ float rowv[9 * 512];
   __shared__ float red[256];
   float m = 0.0f;
-  if (wx) {
-    // (k channel, kernel row dy) pairs: the kernel row's three taps -> its four U values (fp64, rounded
-    // once), stored at k = ((kc / 16) * 3 + dy) * 4 + q) * 16 + kc % 16 with q = 0, 2, 1, 3 for xi = 0..3
-    // (the two planes a step of selunet_conv3x3_wx2 multiplies are adjacent); fwd: row o, k channel c of
-    // w[o][c]; dgrad: row c, k channel o of the flipped kernel (row 2 - dy, taps reversed)
-    const int kdim = fw ? ci : co;
-    for (int j = threadIdx.x; j < 3 * kdim; j += 256) {
-      const int kc = j / 3, dy = j - kc * 3;
-      const float* gw = fw ? w + ((int64_t)row * ci + kc) * 9 + dy * 3 : w + ((int64_t)kc * ci + row) * 9 + (2 - dy) * 3;
-      const double g0 = fw ? gw[0] : gw[2], g1 = gw[1], g2 = fw ? gw[2] : gw[0];
-      const double u[4] = {g0, 0.5 * (g0 + g1 + g2), 0.5 * (g0 - g1 + g2), g2};
-      const int kb = (((kc >> 4) * 3 + dy) * 4) * 16 + (kc & 15);
-#pragma unroll
-      for (int xi = 0; xi < 4; ++xi) {
-        const float v = (float)u[xi];
-        rowv[kb + ((xi & 1) * 2 + (xi >> 1)) * 16] = v;  // planes in the order 0, 2, 1, 3
-        m = fmaxf(m, fabsf(v));
-      }
-    }
-  }
-  for (int j = threadIdx.x; j < (wx ? 0 : len); j += 256) {
+  for (int j = threadIdx.x; j < len; j += 256) {
     int k;
     int64_t src;
     if (ct) {
@@ -240,7 +219,7 @@ __global__ void __launch_bounds__(256) pack_x2_kernel(selunet_pack_list l) {
   float unscale;
   const float sc = x2_scale(red[0], &unscale);
   _Float16* out = reinterpret_cast<_Float16*>(base + (int64_t)row * len);
-  const int gsh = wx ? 4 : 5;  // k groups of 16 (Winograd) or 32 values: high parts, then low parts
+  constexpr int gsh = 5;  // k groups of 32 values: high parts, then low parts
   for (int k = threadIdx.x; k < len; k += 256) {
     const float v = rowv[k] * sc;
     const _Float16 h = (_Float16)v;
@@ -1642,16 +1621,7 @@ int selunet_pack_weights(const selunet_pack_list* list, int32_t dtype, void* str
     selunet_pack_desc& d = l.d[t];
     SELUNET_REQUIRE(d.w && (d.fwd || d.dgrad) && d.co > 0 && d.ci > 0, "pack_weights: bad entry %d", t);
     d.offset = off;
-    if (d.kind == SELUNET_PACK_CONV3X3_WX2) {
-      SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == 12 * d.ci && d.ci % 16 == 0 && d.co % 16 == 0 &&
-                          d.ci <= 512 && d.co <= 512,
-                      "pack_weights: split-fp16 Winograd entry %d needs fp32, fwd, k_pad = 12*ci and ci, co "
-                      "multiples of 16 up to 512", t);
-      lx.d[lx.n] = d;
-      lx.d[lx.n].offset = xrows;
-      ++lx.n;
-      xrows += d.co + (d.dgrad ? d.ci : 0);
-    } else if (d.kind == SELUNET_PACK_CONV3X3_X2 || d.kind == SELUNET_PACK_CONVT_X2) {
+    if (d.kind == SELUNET_PACK_CONV3X3_X2 || d.kind == SELUNET_PACK_CONVT_X2) {
       const bool ct = d.kind == SELUNET_PACK_CONVT_X2;
       SELUNET_REQUIRE(dtype == SELUNET_F32 && d.fwd && d.k_pad == (ct ? d.ci : 9 * d.ci) && d.ci % 32 == 0 &&
                           d.co % 32 == 0,
@@ -1752,7 +1722,7 @@ int selunet_graph_capture_end(void* stream, void** exec) {
     return fail(SELUNET_ELAUNCH, "hipStreamEndCapture failed");
   hipGraphExec_t e = nullptr;
   const hipError_t rc = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
+  (void)hipGraphDestroy(g);
   if (rc != hipSuccess) return fail(SELUNET_ELAUNCH, "hipGraphInstantiate failed");
   *exec = e;
   return 0;

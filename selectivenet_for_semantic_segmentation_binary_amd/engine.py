@@ -34,9 +34,9 @@ BN_CENTER_RATIO = (None if os.environ.get("SELUNET_BN_TWOPASS", "0") == "1"
 FIRST_KPAD = 32  # packed K of encoder_layer_1_1 (9 * C_in <= 27), see selunet_first_conv_fwd
 
 
-# split-fp16 ("x2") kernel forms of a 3x3 layer: direct (selunet_conv3x3_x2) or Winograd F(2,3)
-# (selunet_conv3x3_wx2); both read and write the same operand range words
-X2_MODES = ("x2", "wx2")
+# split-fp16 ("x2") kernel form of a 3x3 layer (selunet_conv3x3_x2; a split-fp16 Winograd F(2,3) form was
+# built in round 4 and retired in round 6: slower on every layer)
+X2_MODES = ("x2",)
 
 
 def _rup(a, b):
@@ -272,9 +272,6 @@ class Engine:
             dg = None
             if self._x2_ok(name, ci, co, hw, need_dgrad, training):
                 mode, kpad, kind = "x2", 9 * ci, K.PACK_CONV3X3_X2
-                if self._shape_ok("selunet_conv3x3_wx2_ok", name, ci, co, hw, need_dgrad):
-                    # (forward and data gradient both on the split-fp16 Winograd F(2,3) kernel)
-                    mode, kpad, kind = "wx2", 12 * ci, K.PACK_CONV3X3_WX2
                 fwd = K.keep(torch.empty(co * kpad + co, dtype=torch.float32, device=dev))
                 if need_dgrad:
                     dg = K.keep(torch.empty(ci * (kpad // ci) * co + ci, dtype=torch.float32, device=dev))
@@ -331,7 +328,7 @@ class Engine:
             words = [s.amax for s in srcs]
             if any(wd is None for wd in words):
                 raise RuntimeError("split-fp16 conv: a source without its range word")
-            K.call("selunet_conv3x3_wx2" if mode == "wx2" else "selunet_conv3x3_x2", g, K.ptr(b), n_cols, ep,
+            K.call("selunet_conv3x3_x2", g, K.ptr(b), n_cols, ep,
                    K.ptr(words[0]), K.ptr(words[1]) if len(words) > 1 else None, self.stream)
         elif mode == "wino":
             K.call("selunet_conv3x3_wino", g, K.ptr(b), n_cols, ep, self.stream)

@@ -34,7 +34,6 @@ import torch.nn.functional as F
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
-import selectivenet_for_semantic_segmentation_binary_amd as S  # noqa: E402
 from selectivenet_for_semantic_segmentation_binary_amd.metrics import SegMetrics, mean_iou  # noqa: E402
 from tests import _golden as G  # noqa: E402
 from tests.test_gpu_train import _miou_data  # noqa: E402
@@ -63,20 +62,16 @@ class _NoisyConvF:
         return getattr(F, name)
 
 
-def _cosine(ep, epochs, lr, lr_min):
-    return lr_min + (lr - lr_min) * (1 + np.cos(np.pi * ep / epochs)) / 2
-
-
 def run_torch(d, data, dtype, noise, eps):
     from oracle import unet_b_cpu as O
     (xtr, ltr), (xva, lva) = data
     bs, epochs, lamb = int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
-    cmin = float(d["meta_cosine_min"])
+    cmin = float(d["meta_cosine_min"]) if "meta_cosine_min" in d.files else 0.0
     params, buffers = O.make_state(int(d["meta_seed"]), "RGB", True)
     params = {k: v.detach().to(DEV, dtype).requires_grad_(True) for k, v in params.items()}
     buffers = {k: (v.to(DEV, dtype) if v.is_floating_point() else v.to(DEV)) for k, v in buffers.items()}
     opt = torch.optim.Adam(list(params.values()), lr=1e-3)
-    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=epochs, eta_min=cmin)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=epochs, eta_min=cmin) if cmin > 0 else None
     xt, lt = torch.tensor(xtr, device=DEV, dtype=dtype), torch.tensor(ltr, device=DEV, dtype=dtype)
     tr = SegMetrics(DEV, selective=True, rule="train")
     f_saved = O.F
@@ -84,7 +79,7 @@ def run_torch(d, data, dtype, noise, eps):
         O.F = _NoisyConvF(eps, noise)
     try:
         for ep in range(epochs):
-            if ep > 0:
+            if ep > 0 and sched is not None:
                 sched.step()
             for b0 in range(0, xt.shape[0], bs):
                 x, lab = xt[b0:b0 + bs], lt[b0:b0 + bs]
@@ -107,22 +102,8 @@ def run_torch(d, data, dtype, noise, eps):
 
 
 def run_hip(d, data, member):
-    from tests.test_gpu_model import build
-    from tests.test_gpu_train import _loop
-    (xtr, ltr), (xva, lva) = data
-    if member:  # make_golden.py _perturbed: 1e-7 N(0,1) relative on the training inputs
-        rng = np.random.Generator(np.random.PCG64(1000 + member))
-        xtr = (xtr.astype(np.float64) * (1.0 + 1e-7 * rng.standard_normal(xtr.shape))).astype(np.float32)
-    bs, ep, lamb = int(d["meta_bs"]), int(d["meta_epochs"]), int(d["meta_lamb"])
-    net = build(True, int(d["meta_seed"]), torch.float32)
-    tr = SegMetrics(DEV, selective=True, rule="train")
-    losses = _loop(net, torch.tensor(xtr, device=DEV), torch.tensor(ltr, device=DEV), bs, ep, lamb, True, [tr],
-                   float(d["meta_cosine_min"]))
-    net.eval()
-    vs, vp = SegMetrics(DEV, selective=True, rule="train"), SegMetrics(DEV, selective=False, rule="train")
-    with torch.no_grad():
-        _loop(net, torch.tensor(xva, device=DEV), torch.tensor(lva, device=DEV), bs, 1, lamb, False, [vs, vp])
-    return tr, vs, vp, float(losses[-1])
+    from tests.test_gpu_train import miou_run
+    return miou_run(d, data, torch.float32, member)
 
 
 def main():
@@ -145,15 +126,15 @@ def main():
         t0 = time.time()
         if a.impl == "torch":
             tr, vs, vp, last = run_torch(d, data, torch.float64 if a.dtype == "f64" else torch.float32, k, a.eps)
+            sel, total = vs.selected_total()
+            rec = {"fixture": a.fixture, "impl": tag, "dtype": a.dtype, "conv_noise": k, "eps": a.eps,
+                   "train_miou": mean_iou(tr.confusion_matrix()), "val_miou": mean_iou(vp.confusion_matrix()),
+                   "val_miou_selective": mean_iou(vs.confusion_matrix()), "val_selected": int(sel),
+                   "val_total": int(total), "last_loss": last}
         else:
-            tr, vs, vp, last = run_hip(d, data, k)
-        sel, total = vs.selected_total()
-        rec = {"fixture": a.fixture, "impl": tag, "dtype": a.dtype if a.impl == "torch" else "f32",
-               "conv_noise" if a.impl == "torch" else "member": k, "eps": a.eps if a.impl == "torch" else 0.0,
-               "train_miou": mean_iou(tr.confusion_matrix()), "val_miou": mean_iou(vp.confusion_matrix()),
-               "val_miou_selective": mean_iou(vs.confusion_matrix()), "val_selected": int(sel),
-               "val_total": int(total), "last_loss": last, "ref_val_miou": float(d["val_miou"]),
-               "ref_val_miou_selective": float(d["val_miou_selective"]), "seconds": round(time.time() - t0, 1)}
+            rec = {"fixture": a.fixture, "impl": tag, "dtype": "f32", **run_hip(d, data, k)}
+        rec.update(ref_val_miou=float(d["val_miou"]), ref_val_miou_selective=float(d["val_miou_selective"]),
+                   seconds=round(time.time() - t0, 1))
         line = json.dumps(rec)
         print(line, flush=True)
         if a.out:

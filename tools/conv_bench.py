@@ -27,7 +27,7 @@ LAYERS = [
 ]
 
 
-def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False, x2=False, wx2=False):
+def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=False, x2=False):
     dev = "cuda"
     srcs = []
     keep = []
@@ -44,7 +44,7 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
     w = (torch.randn(co, kp, device=dev) * 0.05).to(dt)
     g = K.gather(n, hw, hw, 9, *srcs)
     m = n * hw * hw
-    rows = (K.query("selunet_conv3x3_x2_stats_rows", ctypes.byref(g), co) if (x2 or wx2)
+    rows = (K.query("selunet_conv3x3_x2_stats_rows", ctypes.byref(g), co) if x2
             else K.query("selunet_gemm_stats_rows", ctypes.byref(g), co, K.dtype_code(dt)))
     stats = torch.empty(rows, 2, co, device=dev) if not split else None
     if split:  # as in the step: the ConvTranspose2d bias sums of out0 and its range word
@@ -78,17 +78,7 @@ def run(n, c_srcs, co, hw, transform, split, iters, dt=torch.bfloat16, wino=Fals
         keep.append(amax)
         name = K.query("selunet_conv3x3_x2_kernel_name", ctypes.byref(g), co, ep.mode, ep.split).decode()
 
-    if wx2:  # split-fp16 Winograd F(2,3): [co][12*ci] words + co unscale factors (random: timing only)
-        w = torch.randn(co * 12 * ci + co, device=dev).abs() * 1e-3 + 1e-3
-        amax = torch.full((1,), 8.0, device=dev)
-        keep.append(amax)
-        name = "conv3x3_wx2<f32,%d>" % (128 if co % 128 == 0 else 64)
-
     def call():
-        if wx2:
-            K.call("selunet_conv3x3_wx2", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.ptr(amax), K.ptr(amax),
-                   K.stream_ptr())
-            return
         if x2:
             K.call("selunet_conv3x3_x2", ctypes.byref(g), K.ptr(w), co, ctypes.byref(ep), K.ptr(amax), K.ptr(amax),
                    K.stream_ptr())
@@ -175,10 +165,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--wino", action="store_true", help="fp32 Winograd F(2,3) kernel (direct-conv FLOPs reported)")
     ap.add_argument("--x2", action="store_true", help="fp32 on split-fp16 operands (selunet_conv3x3_x2)")
-    ap.add_argument("--wx2", action="store_true", help="fp32 split-fp16 Winograd F(2,3) (selunet_conv3x3_wx2)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    if a.wino or a.x2 or a.wx2:
+    if a.wino or a.x2:
         dt = torch.float32  # (fp32 operands: the kernels read the sources as fp32)
     sel = set(a.layers.split(",")) if a.layers else None
     tot_ms, tot_fl = 0.0, 0.0
@@ -186,7 +175,7 @@ def main():
         if sel and name not in sel:
             continue
         if a.only not in ("dgrad", "wgrad"):
-            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino, a.x2, a.wx2)
+            ms, tf, kn, _ = run(a.batch, (c0, c1), co, hw, True, False, a.iters, dt, a.wino, a.x2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"fwd   {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
@@ -197,7 +186,7 @@ def main():
             print(f"wgrad {name:8s} {c0 + c1:4d}->{co:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)
             continue
         if a.only != "fwd":
-            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino, a.x2, a.wx2)
+            ms, tf, kn, _ = run(a.batch, (co, 0), c0 + c1, hw, False, c1 > 0, a.iters, dt, a.wino, a.x2)
             tot_ms += ms
             tot_fl += tf * ms
             print(f"dgrad {name:8s} {co:4d}->{c0 + c1:4d} @{hw:3d}  {ms:7.3f} ms {tf:7.1f} TF/s  {kn}", flush=True)

@@ -36,7 +36,6 @@ NAME_MAP = [
     (r"conv3x3_x2d_kernel", "conv3x3_x2d<f32,64>"),
     (r"convt_bf16_kernel(<\d+, \d+, false>|ILi\d+ELi\d+ELb0E)", "convt<bf16>"),
     (r"convt_bf16_kernel(<\d+, \d+, true>|ILi\d+ELi\d+ELb1E)", "convt_dgrad<bf16>"),
-    (r"conv3x3_wx2_kernel", "conv3x3_wx2<f32>"),
     (_pat("conv3x3_wgrad_x2_kernel", 128), "conv3x3_wgrad_x2<128>"),
     (_pat("conv3x3_wgrad_x2_kernel", 64), "conv3x3_wgrad_x2<64>"),
 ]
