@@ -60,6 +60,10 @@ enum {
   SELUNET_OPT_TILE_QUEUE,         /* split-fp16 persistent 3x3 kernel: pixel tiles from a ticket counter, statistics
                                    * per tile (1), or the static walk (0, default); selunet_conv3x3_x2_stats_rows
                                    * follows it (robustness to a concurrent all-reduce) */
+  SELUNET_OPT_X2P,                /* 128-column split-fp16 3x3 layers (multi-chunk inputs) on the kernel with two
+                                   * 256-thread workgroups per CU and LDS-DMA weights (1) or on the
+                                   * one-workgroup-per-CU persistent kernel (0, default: measured faster);
+                                   * selunet_conv3x3_x2_stats_rows follows it */
   SELUNET_OPT_CONVT_RING,         /* ConvTranspose2d forward / data gradient on 256-column blocks (fp32: K >= 256;
                                    * bf16: K >= 512): the LDS-DMA ring kernels with the forward on 8 x 1 waves (2,
                                    * default) or, fp32, 4 x 2 waves (1), or the resident-weight / staged kernels (0);

@@ -251,7 +251,7 @@ def load(auto_build: bool = False):
 OPT = {name: i for i, name in enumerate([
     "HALO", "HALO_PERSIST", "WINO", "WINO_WGRAD", "WINO_WGRAD_TW", "WINO_WGRAD_WAVES", "WGRAD_WGS",
     "X2_WGRAD_WGS", "GEMM_WGRAD_WGS", "GATHER_WGS", "RF_SINGLE", "APPLY_U8", "APPLY_GRID", "X2D",
-    "TILE_QUEUE", "CONVT_RING"])}
+    "TILE_QUEUE", "X2P", "CONVT_RING"])}
 # environment variables the host maps onto options at load (A/B and ablation runs of tools/ and the
 # exact-fp32 comparison paths of the tests); SELUNET_NO_HALO=1 means HALO=0
 ENV_OPTIONS = {f"SELUNET_{k}": v for k, v in OPT.items() if k != "HALO"}

@@ -2482,6 +2482,7 @@ static unsigned* tq_counters(hipStream_t st) {
 
 // statistics slab rows of selunet_conv3x3_x2 (persistent kernel): workgroups per column tile, or pixel tiles
 int64_t conv3x3_x2_persist_rows(const GatherArg& g, int N) {
+  if (conv3x3_x2p_eligible(g, N)) return conv3x3_x2p_rows(g, N);
   return x2_tile_queue() ? conv3x3_halo_tiles(g) : persist_rows(g, N);
 }
 
@@ -2520,6 +2521,7 @@ bool conv3x3_x2_bn128(int N, const EpiArg& ep) {
 int conv3x3_x2_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
                       const float* amax1, hipStream_t st) {
   if (conv3x3_x2d_eligible(g, N)) return conv3x3_x2d_launch(g, w, ep, amax0, amax1, st);  // 64 columns
+  if (conv3x3_x2p_eligible(g, N)) return conv3x3_x2p_launch(g, w, N, ep, amax0, amax1, st);  // 128, two per CU
   if (int rc = conv3x3_x2_bn128(N, ep) ? launch_x2<128>(g, w, N, ep, amax0, amax1, st)
                                        : launch_x2<64>(g, w, N, ep, amax0, amax1, st))
     return rc;

@@ -1235,6 +1235,7 @@ extern "C" const char* selunet_conv3x3_x2_kernel_name(const selunet_gather* a, i
   GatherArg g;
   if (make_gather(a, SELUNET_F32, g, 4)) return "?";
   if (conv3x3_x2d_eligible(g, n_cols)) return "conv3x3_x2d<f32,64>";
+  if (conv3x3_x2p_eligible(g, n_cols)) return "conv3x3_x2p<f32,128>";
   return conv3x3_x2_bn128(n_cols, e) ? "conv3x3_x2<f32,128>" : "conv3x3_x2<f32,64>";
 }
 

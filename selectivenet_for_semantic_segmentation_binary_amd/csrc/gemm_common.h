@@ -498,6 +498,11 @@ int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t*
 int conv3x3_wgrad_x2_bi(const GatherArg& p, bool bn);
 // SELUNET_OPT_TILE_QUEUE and the split-fp16 persistent kernel's statistics slab rows (conv3x3.hip)
 bool x2_tile_queue();
+// the 128-column split-fp16 3x3 kernel with two 256-thread workgroups per CU (conv3x3_x2p.hip)
+bool conv3x3_x2p_eligible(const GatherArg& g, int N);
+int64_t conv3x3_x2p_rows(const GatherArg& g, int N);
+int conv3x3_x2p_launch(const GatherArg& g, const float* w, int N, const EpiArg& ep, const float* amax0,
+                       const float* amax1, hipStream_t st);
 int64_t conv3x3_x2_persist_rows(const GatherArg& g, int N);
 // the BN-backward apply fused into the split-fp16 weight gradient's dY staging (selunet_conv3x3_wgrad_x2_bn)
 struct WgradBnArg {

@@ -12,8 +12,8 @@ namespace selunet {
 // ------------------------------------------------------------------ error state, options
 static thread_local char g_err[512] = "";
 
-int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-static_assert(SELUNET_OPT_COUNT == 16, "g_options initialiser: one -1 per option");
+int64_t g_options[SELUNET_OPT_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(SELUNET_OPT_COUNT == 17, "g_options initialiser: one -1 per option");
 
 void set_error(const char* fmt, ...) {
   va_list ap;

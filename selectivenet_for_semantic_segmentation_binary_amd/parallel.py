@@ -86,6 +86,8 @@ class OverlapEmulation:
         ev.record(torch.cuda.current_stream(t.device))
         self.side.wait_event(ev)
         n = (t.numel() // 4) * 4
+        if n == 0:  # (a bucket under 4 floats: nothing the 16-B reduce-copy could read in bounds)
+            return
         us = self.us if self.model is None else self.model[0] + t.numel() * 4 / (self.model[1] * 1e3)
         self.held_us += us
         with torch.cuda.stream(self.side):
@@ -93,7 +95,7 @@ class OverlapEmulation:
             if self.timing:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(self.side)
-            K.call("selunet_cu_hold", K.ptr(t), K.ptr(self.scratch), max(n, 4), self.n_wg, us,
+            K.call("selunet_cu_hold", K.ptr(t), K.ptr(self.scratch), n, self.n_wg, us,
                    self.side.cuda_stream)
             if self.timing:
                 e1.record(self.side)

@@ -35,14 +35,17 @@ def x2d():
 
 @pytest.fixture
 def tile_queue():
-    """Set SELUNET_OPT_TILE_QUEUE for one test (1: tiles from a ticket counter, statistics per tile)."""
+    """The 128-column kernel variant for one test: 0 the static persistent walk, 1 SELUNET_OPT_TILE_QUEUE (tiles
+    from a ticket counter, statistics per tile), 2 SELUNET_OPT_X2P (conv3x3_x2p_kernel: two 256-thread workgroups
+    per CU, LDS-DMA weights; default off, measured slower — kept tested)."""
     prev = []
 
     def setter(mode):
-        prev.append(K.set_option("TILE_QUEUE", mode))
+        prev.append((K.set_option("TILE_QUEUE", 1 if mode == 1 else 0), K.set_option("X2P", 1 if mode == 2 else 0)))
     yield setter
-    for v in prev[:1]:
-        K.set_option("TILE_QUEUE", v)
+    for tq, xp in prev[:1]:
+        K.set_option("TILE_QUEUE", tq)
+        K.set_option("X2P", xp)
 
 
 def pack_x2(w, dgrad=True):
@@ -107,7 +110,7 @@ def word(v):
     (64, 64, 64, 1, 40, 72, True),      # 64 columns, two sources, partial tiles, four chunks
 ])
 @pytest.mark.parametrize("wgs", [0, 3])
-@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1), (0, 2)])
 def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, tq, halo_wgs, x2d, tile_queue):
     halo_wgs(wgs)
     x2d(x2d_mode)
@@ -152,7 +155,7 @@ def test_x2_fwd_stats(cin0, cin1, cout, n, h, w, xform, wgs, x2d_mode, tq, halo_
                                                 (512, 256, 256, 16, 16), (64, 64, 0, 64, 48),
                                                 (64, 128, 0, 48, 40)])
 @pytest.mark.parametrize("wgs", [0, 3])
-@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("x2d_mode,tq", [(1, 0), (0, 0), (0, 1), (0, 2)])
 def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, tq, halo_wgs, x2d, tile_queue):
     """Gradient-sized operands (1e-9 scale): the range word rescales them into the fp16 range."""
     halo_wgs(wgs)

@@ -34,6 +34,7 @@ NAME_MAP = [
     (_pat("conv3x3_halo_persist_kernel", "f32", 128, "true"), "conv3x3_x2<f32,128>"),
     (_pat("conv3x3_halo_persist_kernel", "f32", 64, "true"), "conv3x3_x2<f32,64>"),
     (r"conv3x3_x2d_kernel", "conv3x3_x2d<f32,64>"),
+    (r"conv3x3_x2p_kernel", "conv3x3_x2p<f32,128>"),
     (r"convt_bf16_kernel(<\d+, \d+, false>|ILi\d+ELi\d+ELb0E)", "convt<bf16>"),
     (r"convt_bf16_kernel(<\d+, \d+, true>|ILi\d+ELi\d+ELb1E)", "convt_dgrad<bf16>"),
     (_pat("conv3x3_wgrad_x2_kernel", 128), "conv3x3_wgrad_x2<128>"),
