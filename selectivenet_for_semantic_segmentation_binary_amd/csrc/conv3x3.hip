@@ -720,10 +720,12 @@ conv3x3_halo_persist_kernel(GatherArg g, const T* __restrict__ B, int N, int k_p
     };
     auto bias_col = [&](int cl) { return n0 + cl; };
     if constexpr (TQ) {
-      // this tile's statistics go to slab row pt_cur (the range word stays per workgroup: one atomic at the end)
+      // this tile's statistics go to slab row pt_cur; the range word stays per workgroup (tracked by the store pass,
+      // one atomic at the end — a null amax in the store pass left it 0, i.e. an operand scale of 2^14 for the
+      // consumer, which overflowed the fp16 split once |values| passed 4: the divergence found in round 6)
       TileStats tt = tile_stats(ep, pt_cur, n0, N);
-      tt.amax = nullptr;
       lds_tile_store_acc<T, TH * TW, BN, HTHREADS>(tile, tid, dst, ep.bias, bias_col, tt, s1, s2, s3, amx);
+      tt.amax = nullptr;
       tile_stats_flush<BN, HTHREADS>(tile, tid, tt, s1, s2, s3, 0.0f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s1[e] = s2[e] = s3[e] = 0;

@@ -9,6 +9,7 @@ Tolerance: 2e-6 of the tensor's max magnitude against the fp64 result, as the fp
 (tests/test_gpu_wino.py): v*2^e = h + l holds 22 significant bits per operand and the three fp16
 products are summed in fp32 accumulators 16 at a time, measured at or below the exact fp32 MFMA's
 error (tools/split_probe.hip: relative RMS 3.8e-7 vs 4.3e-7 at K = 1152)."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -177,9 +178,13 @@ def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, tq, halo_wgs, x2d, tile
         d1 = torch.empty(M, cin - split, device=DEV)
         colsum = torch.empty(rows, split, device=DEV)
         ep = K.Epilogue(K.ptr(d0), K.ptr(d1), None, None, K.EP_SPLIT, split, K.ptr(colsum))
+        word_out = torch.zeros(1, device=DEV)
+        ep.amax = K.ptr(word_out)
         K.call("selunet_conv3x3_x2", g, K.ptr(dg), cin, ep, K.ptr(am), None, K.stream_ptr())
         got = torch.cat((nchw(d0.cpu(), n, h, w), nchw(d1.cpu(), n, h, w)), 1)
         assert rel(colsum.double().sum(0).cpu(), d0.double().sum(0).cpu()) < 1e-6
+        # the range word: the exact max |stored value| over both outputs (every kernel variant)
+        assert word_out.item() == max(d0.abs().max().item(), d1.abs().max().item())
     else:
         dx = torch.empty(M, cin, device=DEV)
         yprev = gen(M, cin, seed=42).to(DEV)
@@ -188,9 +193,12 @@ def test_x2_dgrad(cin, cout, split, h, w, wgs, x2d_mode, tq, halo_wgs, x2d, tile
         slab = torch.empty(rows, 3, cin, device=DEV)
         ep = K.Epilogue(K.ptr(dx), None, None, None, K.EP_PLAIN, 0)
         ep.bnb = K.BnBwdStats(K.ptr(yprev), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), K.ptr(slab))
+        word_out = torch.zeros(1, device=DEV)
+        ep.amax = K.ptr(word_out)
         K.call("selunet_conv3x3_x2", g, K.ptr(dg), cin, ep, K.ptr(am), None, K.stream_ptr())
         got = nchw(dx.cpu(), n, h, w)
         check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
+        assert word_out.item() == dx.abs().max().item()  # the range word: the exact max |stored value|
     torch.cuda.synchronize()
     assert rel(got, ref) < TOL
 
@@ -229,7 +237,42 @@ def test_x2_tile_queue_is_schedule_independent(cin, cout, n, h, w, halo_wgs, x2d
     for o in outs[1:]:
         assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1]) and o[2] == outs[0][2]
     assert not torch.isnan(outs[0][1]).any()
+    # the range word is the exact max |stored value| (round 6: the tile-queue path left it 0)
+    assert outs[0][2] == outs[0][0].abs().max().item() > 0
     check_bnb_sums(slab, dx, yprev, sc, sh, mean, invstd)
+
+
+def test_tile_queue_training_matches_static():
+    """60 training steps at 16 x 256^2 (the 8-GPU shard) with SELUNET_OPT_TILE_QUEUE against the static walk: the
+    per-step losses agree to split-fp16 rounding. (Round 6 found the tile-queue path's range word left at 0: the
+    consumer scaled by 2^14 and its fp16 split overflowed once values passed 4 — after ~45 steps the loss jumped
+    from 0.41 to 1.21, while every single-launch test passed.)"""
+    from selectivenet_for_semantic_segmentation_binary_amd.synthetic import make_batch
+    import selectivenet_for_semantic_segmentation_binary_amd as S
+    from tests.test_gpu_model import build
+    x, lab = make_batch(16, 256, seed=0)
+    xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
+    runs = []
+    for tq in (0, 1):
+        prev = K.set_option("TILE_QUEUE", tq)
+        try:
+            net = build(True)
+            opt = S.Adam(net.parameters(), lr=1e-3)
+            la = S.BCEWithLogitsLoss()
+            losses = []
+            for _ in range(60):
+                o, sel, a = net(xt)
+                loss = la(a, lt) + S.calc_selective_risk_image_b(o, sel, target=lt, lamb=2)[0]
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                losses.append(float(loss.item()))
+            runs.append(np.array(losses))
+        finally:
+            K.set_option("TILE_QUEUE", prev)
+    dev = np.abs(runs[1] - runs[0]) / np.abs(runs[0])
+    print(f"tile queue vs static over 60 steps: max relative loss deviation {dev.max():.2e}")
+    assert dev.max() < 1e-3, (dev.argmax(), runs[0][dev.argmax()], runs[1][dev.argmax()])
 
 
 def test_x2_rejects():
