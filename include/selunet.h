@@ -57,9 +57,12 @@ enum {
   SELUNET_OPT_X2D,                /* 64-column split-fp16 3x3 layers on the two-workgroups-per-CU kernel: 0 never,
                                    * 1 every eligible layer, 2 inputs of at most 64 channels, 3 (default) those of
                                    * them whose source carries a BN+ReLU transform (the forwards) */
-  SELUNET_OPT_TILE_QUEUE,         /* split-fp16 persistent 3x3 kernel: pixel tiles from a ticket counter, statistics
-                                   * per tile (1), or the static walk (0, default); selunet_conv3x3_x2_stats_rows
-                                   * follows it (robustness to a concurrent all-reduce) */
+  SELUNET_OPT_TILE_QUEUE,         /* bit mask (robustness to a concurrent all-reduce), 0 = static walks
+                                   * (default). Bit 0: the split-fp16 persistent 3x3 kernel takes its pixel tiles from
+                                   * a ticket counter and writes statistics per tile (selunet_conv3x3_x2_stats_rows
+                                   * follows it). Bit 1: so do the split-fp16 weight gradients' (co tile, ci chunk)
+                                   * groups (each partial then sums the tiles its workgroup took: the weight gradient
+                                   * is not bit-reproducible run to run) */
   SELUNET_OPT_X2P,                /* 128-column split-fp16 3x3 layers (multi-chunk inputs) on the kernel with two
                                    * 256-thread workgroups per CU and LDS-DMA weights (1) or on the
                                    * one-workgroup-per-CU persistent kernel (0, default: measured faster);

@@ -1325,12 +1325,20 @@ constexpr int XTH = 8, XTW = 8, XHW = XTW + 2, XHP = (XTH + 2) * XHW, XPIX = XTH
 // (WgradBnArg, gemm_common.h). BNA: 0 no apply; 1 dA from P; 2 dA = route(pooled) + skip of a max-pooled
 // layer (bn_bwd_apply_pool_kernel's dA: the first maximum of relu(y sc + sh) in row-major window order);
 // 3 dA = sum_h w_h g_h of the 1x1 heads (bn_bwd_apply_heads_kernel's). Modes 2 and 3 are BI = 64 only.
-template <int BI, int BNA = 0>
+// TQ (SELUNET_OPT_TILE_QUEUE bit 1): the `splits` workgroups of a (co tile, ci chunk) group take their
+// pixel tiles from the group's ticket counter instead of a fixed run, so a launch whose workgroups cannot all
+// start at once (CUs held by a concurrent RCCL all-reduce) rebalances instead of ending with the late workgroups'
+// whole run. Two tickets are claimed at the start (the next tile's loads are issued before a tile's MFMAs) and one
+// more per tile at its first k-step. A workgroup's partial then sums the tiles it happened to take: the weight
+// gradient is the same sum in another order (not bit-reproducible run to run); dy and max |dy| are unchanged.
+// tq: [2][groups] counters (tickets, finished workgroups), zero between launches (the group's last workgroup
+// resets both).
+template <int BI, int BNA = 0, bool TQ = false>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_chunks, int64_t tiles_per_split,
                         int tiles_x, int tiles_y, int64_t total_tiles, float* __restrict__ ws, int64_t ws_stride,
                         const float* __restrict__ amax_p, const float* __restrict__ amax_q0,
-                        const float* __restrict__ amax_q1, WgradBnArg bn) {
+                        const float* __restrict__ amax_q1, WgradBnArg bn, unsigned* __restrict__ tq = nullptr) {
   constexpr int LDP = BI + 32;                   // dY plane row stride (halves): 16 dwords mod 64
   constexpr int LDX = 64 + 32;                   // halo plane row stride (halves)
   constexpr int TG = BI == 64 ? 2 : 1;           // tap groups
@@ -1365,8 +1373,25 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   const int64_t split = rest / ci_chunks;
   const int i0 = cot * BI;
   const int c0 = cik * 64;
-  const int64_t pt_begin = split * tiles_per_split;
-  const int64_t pt_end = min(total_tiles, pt_begin + tiles_per_split);
+  const int ngroups = co_tiles * ci_chunks, grp = (int)(lb % (unsigned)ngroups);
+  // tiles pt_first, pt_second, ... below pt_stop: static, the split's run; TQ, claimed tickets (>= total: none)
+  __shared__ int tq_slot[2];
+  int pt_first, pt_second, pt_stop;
+  if constexpr (TQ) {
+    if (tid == 0) {
+      const unsigned t = atomicAdd(tq + grp, 2u);
+      tq_slot[0] = (int)min(t, (unsigned)total_tiles);
+      tq_slot[1] = (int)min(t + 1u, (unsigned)total_tiles);
+    }
+    __syncthreads();
+    pt_first = tq_slot[0];
+    pt_second = tq_slot[1];
+    pt_stop = (int)total_tiles;
+  } else {
+    pt_first = (int)(split * tiles_per_split);
+    pt_second = pt_first + 1;
+    pt_stop = (int)min(total_tiles, (int64_t)pt_first + tiles_per_split);
+  }
 
   int xs_src = 0, xc = c0;
   if (Q.nsrc > 1 && xc >= Q.src[0].C) {
@@ -1609,12 +1634,12 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
 #pragma unroll
   for (int t = 0; t < NTAP; ++t) acc[t] = f32x16{};
 
-  if (pt_begin < pt_end) {
-    load_p((int)pt_begin, 0, P_ROUNDS);
-    load_x((int)pt_begin);
+  if (pt_first < pt_stop) {
+    load_p(pt_first, 0, P_ROUNDS);
+    load_x(pt_first);
     __syncthreads();  // coefficients visible
-    store_p((int)pt_begin, 0, 0, P_ROUNDS);
-    store_x((int)pt_begin, 0);
+    store_p(pt_first, 0, 0, P_ROUNDS);
+    store_x(pt_first, 0);
     __syncthreads();
   }
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -1626,20 +1651,23 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   auto tile_loop = [&](auto ntc) __attribute__((always_inline)) {
     constexpr int NTP = decltype(ntc)::value;
     int buf = 0;
-    for (int pt = (int)pt_begin; pt < (int)pt_end; ++pt) {
-      const bool more = pt + 1 < (int)pt_end;
+    int pt_tq = pt_second;  // TQ: the next tile's ticket
+    for (int pt = pt_first; pt < pt_stop;) {
+      const int ptn = TQ ? pt_tq : pt + 1;  // the next tile
+      const bool more = ptn < pt_stop;
+      unsigned claimed = 0;  // TQ: the ticket tid 0 claims during this tile (the tile after next)
       // the next tile goes to the free buffer in two halves (dY after k-step 1, the halo at the end),
       // so only one half's staging registers are live at a time (BNA at BI = 128: dA and y in two
       // quarters, stored after k-steps 0 and 2)
       constexpr bool QSPLIT = BNA && BI == 128;
       constexpr int PH = QSPLIT ? P_ROUNDS / 2 : P_ROUNDS;
-      load_p(more ? pt + 1 : pt, 0, PH);
+      load_p(more ? ptn : pt, 0, PH);
       __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
 #pragma unroll
       for (int ks = 0; ks < XPIX / 16; ++ks) {  // two tile rows (16 pixels) per k-step
         if (QSPLIT && ks == 1) {
-          if (more) store_p(pt + 1, buf ^ 1, 0, PH);
-          load_p(more ? pt + 1 : pt, PH, P_ROUNDS);
+          if (more) store_p(ptn, buf ^ 1, 0, PH);
+          load_p(more ? ptn : pt, PH, P_ROUNDS);
           __builtin_amdgcn_sched_barrier(0);
         }
         // (QSPLIT: the second dY half is stored at k-step 3, two k-steps after its loads, and the halo's loads get
@@ -1648,13 +1676,16 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
         // the halo loaded at k-step 1 and the dY tile stored at k-step 3, three k-steps of cover each: 3-4 %,
         // profiles/r05q_wgrad64_schedule_ab.txt)
         if (BI == 64 && ks == 1) {
-          load_x(more ? pt + 1 : pt);
+          load_x(more ? ptn : pt);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (ks == (QSPLIT || BI == 64 ? 3 : 2)) {
-          if (more) store_p(pt + 1, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
-          if (BI != 64) load_x(more ? pt + 1 : pt);
+          if (more) store_p(ptn, buf ^ 1, QSPLIT ? PH : 0, P_ROUNDS);
+          if (BI != 64) load_x(more ? ptn : pt);
           __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (TQ) {
+          if (ks == 0 && tid == 0) claimed = atomicAdd(tq + grp, 1u);
         }
         const int prow = ks * 16 + 8 * half + q4;
         const int pcol = wi * 32 + 16 * grp_hi + 4 * p4;
@@ -1692,8 +1723,13 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
           }
         }
       }
-      if (more) store_x(pt + 1, buf ^ 1);
+      if constexpr (TQ) {
+        if (tid == 0) tq_slot[buf] = (int)min(claimed, (unsigned)pt_stop);  // read after the barrier
+      }
+      if (more) store_x(ptn, buf ^ 1);
       __syncthreads();
+      if constexpr (TQ) pt_tq = tq_slot[buf];
+      pt = ptn;
       buf ^= 1;
     }
   };
@@ -1704,6 +1740,14 @@ conv3x3_wgrad_x2_kernel(GatherArg P, GatherArg Q, int ldo, int co_tiles, int ci_
   if constexpr (BNA) {
     // the exact max |dy| of the stored dy: one atomic per workgroup (uniform branch)
     if (bn.dy_amax) block_amax(bn.dy_amax, dam, Ks);
+  }
+  if constexpr (TQ) {
+    const unsigned splits = gridDim.x / (unsigned)ngroups;
+    if (tid == 0 && atomicAdd(tq + ngroups + grp, 1u) == splits - 1u) {
+      // every workgroup of this group has made its last claim: reset for the next launch
+      atomicExch(tq + grp, 0u);
+      atomicExch(tq + ngroups + grp, 0u);
+    }
   }
   const float ofac = uns_p * uns_x;
   const int ctot = Q.Ctot;
@@ -2259,6 +2303,10 @@ int64_t conv3x3_wgrad_x2_splits(const GatherArg& p, const GatherArg& q, int64_t*
   return cdiv(total, per);
 }
 
+static unsigned* tq_counters(hipStream_t st);
+// SELUNET_OPT_TILE_QUEUE bit 1: the split-fp16 weight gradients take their pixel tiles from ticket counters
+static bool x2_wgrad_tile_queue() { return (option(SELUNET_OPT_TILE_QUEUE, 0) & 2) != 0; }
+
 int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, int ldo, const float* amax_p,
                             const float* amax_q0, const float* amax_q1, hipStream_t st, const WgradBnArg* bn) {
   const int bi = conv3x3_wgrad_x2_bi(p, bn != nullptr);
@@ -2270,12 +2318,25 @@ int conv3x3_wgrad_x2_launch(const GatherArg& p, const GatherArg& q, float* ws, i
   const unsigned blocks = (unsigned)(co_tiles * ci_chunks * splits);
   const int kind = bn ? bn->kind : -1;
   SELUNET_REQUIRE(kind <= SELUNET_DA_TENSOR || bi == 64, "conv3x3_wgrad_x2: pool / heads dA sources need 64 columns");
+  if (x2_wgrad_tile_queue()) {  // (co tile, ci chunk) groups take their pixel tiles from ticket counters
+    unsigned* tq = tq_counters(st);
+    if (tq == nullptr || co_tiles * ci_chunks > 64)
+      return fail(SELUNET_ELAUNCH, "conv3x3_wgrad_x2: tile-queue counters unavailable (set SELUNET_OPT_TILE_QUEUE "
+                                   "before capturing the step) or more than 64 (co tile, ci chunk) groups");
+    auto k = bi == 128 ? (bn ? conv3x3_wgrad_x2_kernel<128, 1, true> : conv3x3_wgrad_x2_kernel<128, 0, true>)
+             : kind == SELUNET_DA_POOL  ? conv3x3_wgrad_x2_kernel<64, 2, true>
+             : kind == SELUNET_DA_HEADS ? conv3x3_wgrad_x2_kernel<64, 3, true>
+             : (bn ? conv3x3_wgrad_x2_kernel<64, 1, true> : conv3x3_wgrad_x2_kernel<64, 0, true>);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(512), 0, st, p, q, ldo, co_tiles, ci_chunks, per, tiles_x, tiles_y,
+                       total, ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1, bn ? *bn : WgradBnArg{}, tq);
+    return check_launch("conv3x3_wgrad_x2");
+  }
   auto k = bi == 128 ? (bn ? conv3x3_wgrad_x2_kernel<128, 1> : conv3x3_wgrad_x2_kernel<128, 0>)
            : kind == SELUNET_DA_POOL  ? conv3x3_wgrad_x2_kernel<64, 2>
            : kind == SELUNET_DA_HEADS ? conv3x3_wgrad_x2_kernel<64, 3>
            : (bn ? conv3x3_wgrad_x2_kernel<64, 1> : conv3x3_wgrad_x2_kernel<64, 0>);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(512), 0, st, p, q, ldo, co_tiles, ci_chunks, per, tiles_x, tiles_y, total,
-                     ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1, bn ? *bn : WgradBnArg{});
+                     ws, (int64_t)p.K * ldo, amax_p, amax_q0, amax_q1, bn ? *bn : WgradBnArg{}, nullptr);
   return check_launch("conv3x3_wgrad_x2");
 }
 
@@ -2449,7 +2510,7 @@ bool conv3x3_x2_eligible(const GatherArg& g, int N) {
 
 // SELUNET_OPT_TILE_QUEUE: the split-fp16 persistent kernel takes its pixel tiles from a ticket counter
 // (conv3x3_halo_persist_kernel, TQ) and flushes statistics per tile (slab rows = pixel tiles)
-bool x2_tile_queue() { return option(SELUNET_OPT_TILE_QUEUE, 0) != 0; }
+bool x2_tile_queue() { return (option(SELUNET_OPT_TILE_QUEUE, 0) & 1) != 0; }
 
 // the queue's counters: [2][n_tiles <= 64] per device, zero between launches (each launch's last workgroups
 // reset them). Allocated by selunet_set_option(SELUNET_OPT_TILE_QUEUE, > 0) on the current device — outside

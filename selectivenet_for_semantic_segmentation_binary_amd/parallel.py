@@ -68,9 +68,11 @@ class OverlapEmulation:
     the bucket and reduce-copies into a scratch buffer, so the gradients are untouched. `events`
     collects (bucket elements, start, end) HIP event pairs on the side stream when timing is on."""
 
-    def __init__(self, n_wg: int, us: float, timing: bool = False, model: tuple | None = None):
-        # model (alpha_us, beta_GBs): hold each bucket's CUs for alpha + bytes / beta instead of `us`
+    def __init__(self, n_wg: int, us: float, timing: bool = False, model: tuple | None = None, priority: int = 0):
+        # model (alpha_us, beta_GBs): hold each bucket's CUs for alpha + bytes / beta instead of `us`;
+        # priority: the side stream's (-1 = high, as ProcessGroupNCCL's streams with is_high_priority_stream)
         self.n_wg, self.us, self.timing, self.model = int(n_wg), float(us), timing, model
+        self.priority = int(priority)
         self.held_us = 0.0
         self.side = None
         self.scratch = None
@@ -79,7 +81,7 @@ class OverlapEmulation:
     def launch(self, t: torch.Tensor):
         from . import _lib as K
         if self.side is None:
-            self.side = torch.cuda.Stream(device=t.device)
+            self.side = torch.cuda.Stream(device=t.device, priority=self.priority)
         if self.scratch is None or self.scratch.numel() < t.numel() + 4:
             self.scratch = torch.zeros(t.numel() + 4, dtype=torch.float32, device=t.device)
         ev = torch.cuda.Event()

@@ -249,18 +249,29 @@ def test_wgrad_x2_bn_equals_apply_then_wgrad(co, ci):
     dw0 = torch.empty(co, ci, 3, 3, device=DEV)
     K.call("selunet_conv3x3_wgrad_x2", gp0, gq, K.ptr(ws), wsb, K.ptr(dw0), K.ptr(am0), K.ptr(xw), None, K.stream_ptr())
     torch.cuda.synchronize()
-    # fused
+    # fused (static walk, then SELUNET_OPT_TILE_QUEUE bit 1: tiles from ticket counters — dy and max |dy| are the
+    # same element-wise arithmetic, the weight gradient the same sum in another order)
     bound = (am0 * 37.0).contiguous()
-    dy1 = torch.full((m, co), float("nan"), device=DEV)
-    am1 = torch.zeros(1, device=DEV)
-    dw1 = torch.empty(co, ci, 3, 3, device=DEV)
     gp1 = K.gather(n, h, w, 1, K.source(da, co))
     bnb = K.BnBwdStats(K.ptr(y), K.ptr(sc), K.ptr(sh), K.ptr(mean), K.ptr(invstd), None)
-    K.call("selunet_conv3x3_wgrad_x2_bn", gp1, gq, K.ptr(ws), wsb, K.ptr(dw1), K.ptr(bound), K.ptr(xw), None, bnb,
-           K.ptr(coef), K.ptr(dy1), K.ptr(am1), K.stream_ptr())
-    torch.cuda.synchronize()
-    assert torch.equal(dy1.cpu(), dy0.cpu())
-    assert am1.item() == am0.item()
+    fused = []
+    prev = K.set_option("TILE_QUEUE", 0)
+    try:
+        for tq in (0, 2):
+            K.set_option("TILE_QUEUE", tq)
+            dy1 = torch.full((m, co), float("nan"), device=DEV)
+            am1 = torch.zeros(1, device=DEV)
+            dw1 = torch.empty(co, ci, 3, 3, device=DEV)
+            K.call("selunet_conv3x3_wgrad_x2_bn", gp1, gq, K.ptr(ws), wsb, K.ptr(dw1), K.ptr(bound), K.ptr(xw), None,
+                   bnb, K.ptr(coef), K.ptr(dy1), K.ptr(am1), K.stream_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(dy1.cpu(), dy0.cpu()), tq
+            assert am1.item() == am0.item(), tq
+            fused.append(dw1.cpu())
+    finally:
+        K.set_option("TILE_QUEUE", prev)
+    assert float((fused[1].double() - fused[0].double()).norm() / fused[0].double().norm()) < 1e-6
+    dw1 = fused[0]
     # fp64 weight gradient of dy0 against relu(x sc + sh)
     xin = torch.relu(x.double() * xsc.double() + xsh.double()).reshape(n, h, w, ci).permute(0, 3, 1, 2)
     g = dy0.double().reshape(n, h, w, co).permute(0, 3, 1, 2)

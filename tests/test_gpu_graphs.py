@@ -63,3 +63,28 @@ def test_graph_replay_tile_queue(monkeypatch):
             assert np.array_equal(a["grads"][k], b["grads"][k]), (s, k)
     for k in p_g:
         assert np.array_equal(p_g[k], p_e[k]), k
+
+
+def test_graph_replay_tile_queue_wgrad(monkeypatch):
+    """SELUNET_OPT_TILE_QUEUE = 3 (the weight gradients' ticket counters too) under graph capture: the step runs
+    captured, and matches per-launch replay to rounding — the weight-gradient partials sum the tiles each
+    workgroup took, so bit equality is not expected. The first step's gradients are compared element-wise; later
+    steps by their loss only (Adam's first update is ~lr sign(g) per element, so rounding-level gradient
+    differences where g ~ 0 become lr-sized parameter differences)."""
+    from selectivenet_for_semantic_segmentation_binary_amd import _lib as K
+    prev = K.set_option("TILE_QUEUE", 3)
+    try:
+        h_g, p_g, n_g = _run(monkeypatch, True, torch.float32, steps=3)
+        h_e, p_e, _ = _run(monkeypatch, False, torch.float32, steps=3)
+    finally:
+        K.set_option("TILE_QUEUE", prev)
+    assert n_g > 0
+    for s, (a, b) in enumerate(zip(h_g, h_e)):
+        assert abs(a["loss"] - b["loss"]) <= 1e-4 * abs(b["loss"]), (s, a["loss"], b["loss"])
+        if s > 0:
+            continue
+        for k in a["grads"]:
+            if k.endswith(".0.bias"):  # pre-BN conv biases: analytically zero, rounding noise either way
+                continue
+            ga, gb = np.asarray(a["grads"][k], np.float64), np.asarray(b["grads"][k], np.float64)
+            assert np.abs(ga - gb).max() <= 1e-4 * max(np.abs(gb).max(), 1e-30), (s, k)

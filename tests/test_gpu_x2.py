@@ -253,7 +253,7 @@ def test_tile_queue_training_matches_static():
     x, lab = make_batch(16, 256, seed=0)
     xt, lt = torch.tensor(x, device=DEV), torch.tensor(lab, device=DEV)
     runs = []
-    for tq in (0, 1):
+    for tq in (0, 1, 2, 3):  # static, the convolutions' tile queue, the weight gradients', both
         prev = K.set_option("TILE_QUEUE", tq)
         try:
             net = build(True)
@@ -270,9 +270,10 @@ def test_tile_queue_training_matches_static():
             runs.append(np.array(losses))
         finally:
             K.set_option("TILE_QUEUE", prev)
-    dev = np.abs(runs[1] - runs[0]) / np.abs(runs[0])
-    print(f"tile queue vs static over 60 steps: max relative loss deviation {dev.max():.2e}")
-    assert dev.max() < 1e-3, (dev.argmax(), runs[0][dev.argmax()], runs[1][dev.argmax()])
+    for k in (1, 2, 3):
+        dev = np.abs(runs[k] - runs[0]) / np.abs(runs[0])
+        print(f"tile queue {k} vs static over 60 steps: max relative loss deviation {dev.max():.2e}")
+        assert dev.max() < 1e-3, (k, dev.argmax(), runs[0][dev.argmax()], runs[k][dev.argmax()])
 
 
 def test_x2_rejects():
@@ -384,6 +385,50 @@ def test_x2_wgrad(cin0, cin1, cout, xform, n, h, w):
     torch.cuda.synchronize()
     assert rel(outs[0].cpu(), ref) < TOL
     assert torch.equal(outs[0], outs[1])  # fixed-order reduction: bit-reproducible
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(128, 256, 2, 20, 36), (256, 64, 3, 12, 18), (512, 512, 2, 16, 16)])
+def test_x2_wgrad_tile_queue(cin, cout, n, h, w):
+    """SELUNET_OPT_TILE_QUEUE bit 1 (= 2): the weight gradient's (co tile, ci chunk) groups take their pixel tiles from
+    ticket counters. Every tile is summed exactly once whatever the assignment: against the fp64 weight gradient
+    at the split-fp16 tolerance and against the static walk to rounding, under three workgroup targets (one, a
+    few and many workgroups per group) and repeated launches (the counters reset themselves)."""
+    x = gen(n, cin, h, w, seed=31)
+    s0, t0 = bn_fold(cin, 32)
+    a = torch.relu(x * s0.view(1, -1, 1, 1) + t0.view(1, -1, 1, 1))
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    keep = [d(nhwc(x)), d(s0), d(t0)]
+    gq = K.gather(n, h, w, 9, K.source(keep[0], cin, keep[1], keep[2]))
+    wt = gen(cout, cin, 3, 3, seed=33, scale=0.05).double().requires_grad_()
+    dy = gen(n, cout, h, w, seed=34) * 1e-9
+    (ref,) = torch.autograd.grad(F.conv2d(a.double(), wt, padding=1), wt, dy.double())
+    dyd = d(nhwc(dy))
+    amp, am0 = word(dy.abs().max()), word(a.abs().max())
+    gp = K.gather(n, h, w, 1, K.source(dyd, cout))
+    outs = {}
+    prev_tq = K.set_option("TILE_QUEUE", 0)
+    prev_wgs = K.set_option("X2_WGRAD_WGS", 256)
+    try:
+        for tq, wgs in [(0, 256), (2, 256), (2, 64), (2, 2048), (2, 256)]:
+            K.set_option("TILE_QUEUE", tq)
+            K.set_option("X2_WGRAD_WGS", wgs)
+            wsb = K.query("selunet_conv3x3_wgrad_x2_ws_bytes", gp, gq)
+            ws = torch.empty(wsb // 4, device=DEV)
+            out = torch.full((cout, cin, 3, 3), float("nan"), device=DEV)
+            K.call("selunet_conv3x3_wgrad_x2", gp, gq, K.ptr(ws), wsb, K.ptr(out), K.ptr(amp), K.ptr(am0), None,
+                   K.stream_ptr())
+            torch.cuda.synchronize()
+            outs.setdefault((tq, wgs), []).append(out.cpu())
+    finally:
+        K.set_option("TILE_QUEUE", prev_tq)
+        K.set_option("X2_WGRAD_WGS", prev_wgs)
+    static = outs[(0, 256)][0]
+    assert rel(static, ref) < TOL
+    for key, lst in outs.items():
+        for o in lst:
+            assert not torch.isnan(o).any(), key
+            assert rel(o, ref) < TOL, key
+            assert rel(o, static.double()) < 1e-6, key
 
 
 def pack_convT_x2(w):

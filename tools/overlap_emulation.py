@@ -41,6 +41,8 @@ def main():
                     "bucket bytes / beta (a bandwidth model of the all-reduce) instead of the case's fixed us")
     ap.add_argument("--priority", type=int, default=0, help="run the step on a stream of this priority "
                     "(-1: high; the stand-in's side stream stays at the default)")
+    ap.add_argument("--side-priority", type=int, default=0, help="the stand-in's side stream priority (-1: high, "
+                    "as ProcessGroupNCCL.Options(is_high_priority_stream=True) gives RCCL's streams)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -91,7 +93,8 @@ def main():
         for c in cases:
             belems, n_wg, us = c
             parallel.set_bucket_elems(belems)
-            emu = parallel.OverlapEmulation(n_wg, us, timing=True, model=model) if n_wg > 0 else None
+            emu = (parallel.OverlapEmulation(n_wg, us, timing=True, model=model, priority=a.side_priority)
+                   if n_wg > 0 else None)
             parallel.set_overlap_emulation(emu)
             step()  # a fresh plan key is not needed: the markers are host hooks between graph segments
             torch.cuda.synchronize()
@@ -129,14 +132,14 @@ def main():
                "standin_side_ms": round(min(side[c]), 3) if side[c] else 0.0,
                "standin_cu_share_ms": round(held.get(c, 0.0) / 1e3 * n_wg / 256, 3)}
         rows.append(row)
-        print(f"{'model ' + a.model + ' ' if model else ''}prio {a.priority} halo {a.halo_wgs or 256} "
+        print(f"{'model ' + a.model + ' ' if model else ''}prio {a.priority} side {a.side_priority} halo {a.halo_wgs or 256} "
               f"bucket {row['bucket_mb']:5.1f} MB  n_wg {n_wg:3d}  us {us:6.0f}  buckets {nbk:2d}  "
               f"{ms:8.3f} ms/step  inflation {row['inflation_ms']:7.3f} ms  stand-in wall {row['standin_wall_ms']:6.3f} ms "
               f"(side stream {row['standin_side_ms']:6.3f}, CU share {row['standin_cu_share_ms']:6.3f})", flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"batch": a.batch, "steps": a.steps, "options": a.option, "halo_wgs": a.halo_wgs, "model": a.model,
-                       "priority": a.priority, "rows": rows}, f,
+                       "priority": a.priority, "side_priority": a.side_priority, "rows": rows}, f,
                       indent=1)
 
 
