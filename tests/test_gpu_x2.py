@@ -700,3 +700,10 @@ def test_x2_convT_wgrad(cin, cout, n, h, w):
     torch.cuda.synchronize()
     assert rel(outs[0].cpu(), gw) < TOL
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 128, 160), (3, 100, 96), (1, 70, 64)])
+def test_x2_convT_wgrad_deep(n, h, w):
+    """unpool1's shape class (128 x 256 tiles, gemm_wgrad_x2_kernel<128, 256, 512>) over splits of many 32-pixel
+    stages, ragged last stages and odd / even stage counts per split."""
+    test_x2_convT_wgrad(128, 64, n, h, w)
