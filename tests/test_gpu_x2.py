@@ -270,10 +270,13 @@ def test_tile_queue_training_matches_static():
             runs.append(np.array(losses))
         finally:
             K.set_option("TILE_QUEUE", prev)
+    # Rounding-level differences grow along a training trajectory: the deterministic conv queue (1) ends 60 steps
+    # 7.8e-4 from the static walk, the weight-gradient queues (2, 3), whose summation order changes run to run,
+    # 1.1e-3 in one run (r06). The bound is 5e-3 — the failure it guards against moved the loss by a factor 3.
     for k in (1, 2, 3):
         dev = np.abs(runs[k] - runs[0]) / np.abs(runs[0])
         print(f"tile queue {k} vs static over 60 steps: max relative loss deviation {dev.max():.2e}")
-        assert dev.max() < 1e-3, (k, dev.argmax(), runs[0][dev.argmax()], runs[k][dev.argmax()])
+        assert dev.max() < 5e-3, (k, dev.argmax(), runs[0][dev.argmax()], runs[k][dev.argmax()])
 
 
 def test_x2_rejects():
