@@ -80,7 +80,7 @@ def test_graph_replay_tile_queue_wgrad(monkeypatch):
         K.set_option("TILE_QUEUE", prev)
     assert n_g > 0
     for s, (a, b) in enumerate(zip(h_g, h_e)):
-        assert abs(a["loss"] - b["loss"]) <= 1e-4 * abs(b["loss"]), (s, a["loss"], b["loss"])
+        assert abs(a["loss"] - b["loss"]) <= (1e-5 if s == 0 else 1e-3) * abs(b["loss"]), (s, a["loss"], b["loss"])
         if s > 0:
             continue
         for k in a["grads"]:
